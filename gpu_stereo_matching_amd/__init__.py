@@ -1,0 +1,194 @@
+"""MI355X-native stereo block matching (gfx950 HIP kernels behind a C ABI).
+
+Host-side mirror of the reference's GPU proxy API (ningw42/GPU_Stereo_Matching):
+
+    void blockMatching_gpu(Mat &h_left, Mat &h_right, Mat &h_disparity,
+                           int SADWindowSize, int searchRange);      // Device.cuh:50
+
+``blockMatching_gpu(h_left, h_right, SADWindowSize, searchRange)`` takes two uint8 gray
+images (numpy, HxW) and returns the uint8 disparity map, with the reference's argument
+meaning (SADWindowSize = window radius r, window (2r+1)^2; searchRange = number of
+disparities) and output convention (0 where no window SAD is below 50*(2r+1)^2).
+
+``BlockMatcher`` is the handle-based interface (buffers allocated once, device-resident
+batched calls on torch tensors, LR check, guided aggregation, d-slice keys for multi-GPU).
+All compute runs in ``libsm_hip.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _capi
+from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK  # noqa: F401
+from .synth import synth_pair  # noqa: F401
+from .gray import bgr_to_gray  # noqa: F401
+
+__all__ = [
+    "BlockMatcher", "blockMatching_gpu", "block_matching_gpu", "SMError", "synth_pair", "bgr_to_gray",
+    "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "version",
+]
+
+DEFAULT_GUIDED_EPS = 1e-4 * 255.0 * 255.0
+
+
+def version() -> str:
+    return _capi.load().sm_version().decode()
+
+
+def _as_u8_image(a, name: str) -> np.ndarray:
+    a = np.asarray(a)
+    if a.dtype != np.uint8 or a.ndim != 2:
+        raise ValueError(f"{name}: expected a 2-D uint8 (CV_8UC1) image, got {a.dtype} {a.shape}")
+    return a if a.flags.c_contiguous else np.ascontiguousarray(a)
+
+
+def _flags(agg: str, lr_check: bool) -> int:
+    if agg not in ("box", "guided"):
+        raise ValueError("agg must be 'box' or 'guided'")
+    f = SM_AGG_GUIDED if agg == "guided" else SM_AGG_BOX
+    return f | (SM_LR_CHECK if lr_check else 0)
+
+
+class BlockMatcher:
+    """One device handle: pre-allocated buffers + a HIP stream (``sm_create``)."""
+
+    def __init__(self, device: int = 0, max_width: int = 1920, max_height: int = 1080, max_disp: int = 256):
+        self._lib = _capi.load()
+        h = ctypes.c_void_p()
+        _capi.check(self._lib.sm_create(device, max_width, max_height, max_disp, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.max_width, self.max_height, self.max_disp = max_width, max_height, max_disp
+
+    # -- lifetime ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.sm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_guided_eps(self, eps: float):
+        _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_GUIDED_EPS, float(eps)))
+
+    # -- host-pointer path (blockMatching_gpu replacement) -------------------------------
+    def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False) -> np.ndarray:
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        if L.shape != R.shape:
+            raise ValueError("left/right sizes differ")
+        H, W = L.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_block_match_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
+                                                _flags(agg, lr_check), out.ctypes.data, W))
+        return out
+
+    def match_lr(self, left, right, radius: int, num_disp: int, agg: str = "box"
+                 ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(checked disparity, right-view disparity, valid mask)."""
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        H, W = L.shape
+        out = np.empty((H, W), np.uint8)
+        rd = np.empty((H, W), np.uint8)
+        mask = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_block_match_lr_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
+                                                   _flags(agg, True), out.ctypes.data, rd.ctypes.data,
+                                                   mask.ctypes.data, W))
+        return out, rd, mask
+
+    def stage_ms(self) -> Tuple[float, float, float]:
+        """(upload, match, download) ms of the last host call (Device.cu:218,238/257,292)."""
+        u, m, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        _capi.check(self._lib.sm_last_stage_ms(self._h, ctypes.byref(u), ctypes.byref(m), ctypes.byref(d)))
+        return u.value, m.value, d.value
+
+    # -- device-resident path (torch tensors in HBM) ------------------------------------
+    @staticmethod
+    def _stream_ptr(stream):
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream()
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    def match_device(self, left_t, right_t, radius: int, num_disp: int, out_t=None, agg: str = "box",
+                     lr_check: bool = False, stream=None):
+        """left_t/right_t: uint8 cuda tensors [H, W] or [B, H, W] (contiguous). Async on `stream`."""
+        import torch
+        if left_t.dtype != torch.uint8 or right_t.dtype != torch.uint8:
+            raise ValueError("expected uint8 tensors")
+        if left_t.shape != right_t.shape or left_t.dim() not in (2, 3):
+            raise ValueError("left/right must be equal [H,W] or [B,H,W]")
+        if not (left_t.is_cuda and right_t.is_cuda and left_t.is_contiguous() and right_t.is_contiguous()):
+            raise ValueError("expected contiguous device tensors")
+        B = 1 if left_t.dim() == 2 else left_t.shape[0]
+        H, W = left_t.shape[-2:]
+        if out_t is None:
+            out_t = torch.empty_like(left_t)
+        _capi.check(self._lib.sm_match_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, B, H * W,
+                                              radius, num_disp, _flags(agg, lr_check), out_t.data_ptr(), W, H * W,
+                                              self._stream_ptr(stream)))
+        return out_t
+
+    def slice_keys_device(self, left_t, right_t, radius: int, d_lo: int, d_hi: int, keys_t=None, stream=None):
+        """Packed (SAD<<8|d) keys of the d-slice [d_lo, d_hi) as an int32 tensor (bit pattern of uint32)."""
+        import torch
+        H, W = left_t.shape[-2:]
+        if keys_t is None:
+            keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        _capi.check(self._lib.sm_slice_keys_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, radius,
+                                                   d_lo, d_hi, keys_t.data_ptr(), self._stream_ptr(stream)))
+        return keys_t
+
+    def keys_to_disp_device(self, keys_t, radius: int, out_t=None, stream=None):
+        import torch
+        H, W = keys_t.shape[-2:]
+        if out_t is None:
+            out_t = torch.empty((H, W), dtype=torch.uint8, device=keys_t.device)
+        _capi.check(self._lib.sm_keys_to_disp_device(self._h, keys_t.data_ptr(), W, H, radius, out_t.data_ptr(), W,
+                                                     self._stream_ptr(stream)))
+        return out_t
+
+
+_default: Optional[BlockMatcher] = None
+
+
+def _default_matcher(W: int, H: int, D: int) -> BlockMatcher:
+    global _default
+    if _default is None or W > _default.max_width or H > _default.max_height or D > _default.max_disp:
+        if _default is not None:
+            _default.close()
+        _default = BlockMatcher(0, max(W, 1920), max(H, 1080), 256)
+    return _default
+
+
+def blockMatching_gpu(h_left, h_right, SADWindowSize: int, searchRange: int) -> np.ndarray:
+    """Drop-in for ``blockMatching_gpu`` (Device.cu:173): returns the uint8 disparity map.
+
+    Prints the reference's stage lines ("upload data", "pre calculation"/"find corr",
+    "download data" in ms, Device.cu:218,238,257,292) only when ``SM_VERBOSE`` is set.
+    """
+    L = _as_u8_image(h_left, "h_left")
+    m = _default_matcher(L.shape[1], L.shape[0], searchRange)
+    out = m.match(L, h_right, SADWindowSize, searchRange)
+    import os
+    if os.environ.get("SM_VERBOSE"):
+        u, c, d = m.stage_ms()
+        print(f"upload data : {u}\nfind corr : {c}\ndownload data : {d}")
+    return out
+
+
+block_matching_gpu = blockMatching_gpu

@@ -1,0 +1,82 @@
+// bm_aux.hip — byte-streaming kernels around the matcher: key finalisation (multi-GPU
+// d-slice reduction), horizontal mirror (right view), left-right consistency check.
+// All are HBM-bound elementwise passes: 16 pixels per thread, 16-B loads where aligned.
+#include "bm_common.h"
+
+namespace sm {
+namespace {
+
+// key -> disparity (Device.cu:37-38,57,63: d when the best SAD is below 50*win^2, else 0)
+__global__ __launch_bounds__(256) void keys_to_disp_kernel(const uint32_t* __restrict__ keys, int W, int H,
+                                                           uint32_t thresh_key, uint8_t* __restrict__ disp,
+                                                           int out_pitch) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const uint32_t k = keys[(int64_t)y * W + x];
+    disp[(int64_t)y * out_pitch + x] = k < thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
+}
+
+// dst(y, x) = src(y, W-1-x) for each frame
+__global__ __launch_bounds__(256) void mirror_kernel(const uint8_t* __restrict__ src, int W, int H, int pitch,
+                                                     int64_t stride, uint8_t* __restrict__ dst, int dpitch,
+                                                     int64_t dstride) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int f = blockIdx.z;
+    if (x >= W) return;
+    dst[(int64_t)f * dstride + (int64_t)y * dpitch + x] = src[(int64_t)f * stride + (int64_t)y * pitch + (W - 1 - x)];
+}
+
+// StereoDisparity.cpp:136-147 with the right map stored mirrored (index W-1-u holds dR(u)):
+//   d = dL(y,x); occ = x-d < 0 || d == 0 || |d - dR(y, x-d)| > 1;  out = occ ? 0 : d
+__global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* __restrict__ ld, int lpitch, int64_t lstride,
+                                                       const uint8_t* __restrict__ rdm, int rpitch, int64_t rstride,
+                                                       int W, uint8_t* __restrict__ out, int opitch, int64_t ostride,
+                                                       uint8_t* __restrict__ right_out, uint8_t* __restrict__ mask_out,
+                                                       int apitch, int64_t astride) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int f = blockIdx.z;
+    if (x >= W) return;
+    const uint8_t* lrow = ld + (int64_t)f * lstride + (int64_t)y * lpitch;
+    const uint8_t* rrow = rdm + (int64_t)f * rstride + (int64_t)y * rpitch;
+    const int d = lrow[x];
+    int occ = 1;
+    if (x - d >= 0) {
+        const int dr = rrow[W - 1 - (x - d)];
+        const int diff = d - dr;
+        occ = (d == 0) || diff > 1 || diff < -1;
+    }
+    out[(int64_t)f * ostride + (int64_t)y * opitch + x] = occ ? (uint8_t)0 : (uint8_t)d;
+    if (mask_out) mask_out[(int64_t)f * astride + (int64_t)y * apitch + x] = (uint8_t)!occ;
+    if (right_out) right_out[(int64_t)f * astride + (int64_t)y * apitch + x] = rrow[W - 1 - x];
+}
+
+}  // namespace
+
+hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key, uint8_t* disp,
+                               int out_pitch, hipStream_t s) {
+    dim3 grid((W + 255) / 256, H, 1);
+    hipLaunchKernelGGL(keys_to_disp_kernel, grid, dim3(256), 0, s, keys, W, H, thresh_key, disp, out_pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch, uint8_t* dst,
+                         int dst_pitch, int64_t dst_stride, hipStream_t s) {
+    dim3 grid((W + 255) / 256, H, batch);
+    hipLaunchKernelGGL(mirror_kernel, grid, dim3(256), 0, s, src, W, H, pitch, stride, dst, dst_pitch, dst_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride, const uint8_t* right_disp_mirrored,
+                           int rpitch, int64_t rstride, int W, int H, int batch, uint8_t* out, int opitch,
+                           int64_t ostride, uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
+                           hipStream_t s) {
+    dim3 grid((W + 255) / 256, H, batch);
+    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, s, left_disp, lpitch, lstride, right_disp_mirrored,
+                       rpitch, rstride, W, out, opitch, ostride, right_out, mask_out, aux_pitch, aux_stride);
+    return hipGetLastError();
+}
+
+}  // namespace sm

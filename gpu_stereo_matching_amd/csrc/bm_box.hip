@@ -1,0 +1,282 @@
+// bm_box.hip — fused AD + box-window SAD + winner-take-all for gfx950 (CDNA4).
+//
+// Replaces the reference's two-kernel pipeline
+//   kernalPreCal_V2  (BlockMatching/Device.cu:19-32)   AD volume, P*D bytes to HBM
+//   kernalFindCorr   (BlockMatching/Device.cu:34-64)   win^2 byte loads per (pixel, d) + WTA
+// with one kernel that never materialises the AD or SAD volume: per tile the right-image
+// scanline band (block + d_max wide) sits in LDS, vertical window sums run down each column
+// in registers, horizontal window sums run along rows from an LDS hand-off, and the
+// (SAD << 8 | d) argmin is kept per pixel in VGPRs.  Semantics (bit-exact with getDisp,
+// BlockMatching.cpp:111-189):
+//   AD_d(y,c)  = |L(y,c) - R(y,c-d)| for c >= d, else 0            (Device.cu:27-31, :194)
+//   S_d(y,x)   = sum of AD_d over the (2r+1)^2 window clipped to the image (Device.cu:46-56)
+//   valid      = d <= W - x   (the `col + d > cols` break, Device.cu:44)
+//   WTA        = first d with the smallest S_d below 50*win^2, else 0  (Device.cu:37-38,57,63)
+//
+// Tile geometry (R = radius, compile-time for R <= 7):
+//   64 CS columns (one per lane) -> TW = 64 - 2R output columns, TH = 32 output rows.
+//   A chunk of 8 disparities = 4 pairs; wave w owns pair w in both phases.
+//   Phase V (lane = column): T += |L - R_d| in the low u16 and |L - R_{d+1}| in the high u16
+//     (v_sad_u8 / v_sad_hi_u8); CS = T_i - T_{i-2R-1} (column window sums, two d per dword).
+//   Phase H (lane = row x half-row): running window sum along x over the packed pairs, keys
+//     (S << 8 | d) built with v_perm_b32, folded with v_min3_u32.
+#include "bm_common.h"
+
+namespace sm {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTileH = 32;
+constexpr int kPairs = 4;
+constexpr int kChunk = 2 * kPairs;
+constexpr int kCols = 64;
+
+template <int R>
+struct Geo {
+    static constexpr int TW = kCols - 2 * R;                  // output columns per tile
+    static constexpr int ROWS = kTileH + 2 * R;                 // input rows per tile
+    static constexpr int NOUT = (((TW + 1) / 2) + 3) & ~3;      // outputs per phase-H thread
+    static constexpr int NCS4 = (NOUT + 2 * R + 3) / 4;         // 16-B CS reads per phase-H thread
+    static constexpr int NEED = (NOUT + 4 * NCS4) > kCols ? (NOUT + 4 * NCS4) : kCols;
+    // row stride in dwords, == 4 (mod 8) so 16 rows read by one ds_read_b128 lane group hit
+    // 16 distinct 4-bank slots (conflict-free)
+    static constexpr int CSS = (NEED % 8 <= 4) ? NEED + (4 - NEED % 8) : NEED + (12 - NEED % 8);
+    static constexpr int CS_BYTES = kPairs * kTileH * CSS * 4;
+};
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t* p, int y, int x, int W, int H, int pitch) {
+    return (y >= 0 && y < H && x >= 0 && x < W) ? (uint32_t)p[(int64_t)y * pitch + x] : 0u;
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
+    using G = Geo<R>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [kPairs][kTileH][CSS]
+    uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::CS_BYTES);       // [ROWS][RW]
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+
+    const int tiles = tiles_x * tiles_y;
+    const int frame = blockIdx.x / tiles;
+    const int t = blockIdx.x - frame * tiles;
+    const int ty = t / tiles_x;
+    const int tx = t - ty * tiles_x;
+    const int x0 = tx * G::TW;
+    const int y0 = ty * kTileH;
+    const int W = a.W, H = a.H;
+
+    const uint8_t* Lf = a.left + (int64_t)frame * a.frame_stride;
+    const uint8_t* Rf = a.right + (int64_t)frame * a.frame_stride;
+
+    const int d_lo = a.d_lo, d_hi = a.d_hi;
+    const int dspan = (d_hi - d_lo + kChunk - 1) & ~(kChunk - 1);
+    constexpr int RW = kCols + kMaxDisp;           // u16 entries per R row in LDS (fixed: immediate offsets)
+    const int RWU = kCols + dspan;                 // entries actually staged per row
+    const int base = x0 - R - d_lo - dspan;        // image column of rs[.][0]
+
+    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8 ----
+    for (int e = tid; e < G::ROWS * RWU; e += kThreads) {
+        const int i = e / RWU, k = e - i * RWU;
+        const int y = y0 - R + i, c = base + k;
+        const uint32_t v = ld_u8(Rf, y, c, W, H, a.pitch) | (ld_u8(Rf, y, c - 1, W, H, a.pitch) << 8);
+        rs[i * RW + k] = (uint16_t)v;
+    }
+    // ---- this lane's left column, L in bytes 0 and 1 (for the v_bfi operand build) ----
+    const int c = x0 - R + lane;                   // image column of CS column `lane`
+    uint32_t lp[G::ROWS];
+#pragma unroll
+    for (int i = 0; i < G::ROWS; ++i) lp[i] = ld_u8(Lf, y0 - R + i, c, W, H, a.pitch) * 0x0101u;
+
+    // ---- per-thread phase-H state: (row j, half h) of pair `wave` ----
+    const int hj = lane & 31;
+    const int hh = lane >> 5;
+    const int obase = hh * G::NOUT;                // first tile output column of this thread
+    uint32_t best[G::NOUT];
+#pragma unroll
+    for (int o = 0; o < G::NOUT; ++o) best[o] = a.seed_key;
+
+    const bool col_edge = (x0 - R < 0) || (x0 - R + kCols > W) || (x0 - R < d_hi - 1);
+    const int xmax_tile = min(x0 + G::TW, W) - 1;
+    const bool d_edge = a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0);
+
+    __syncthreads();
+
+    for (int d0 = d_lo; d0 < d_lo + dspan; d0 += kChunk) {
+        const int d = d0 + 2 * wave;               // this wave's pair: d, d+1
+        // ================= phase V =================
+        {
+            const uint16_t* rcol = rs + (lane + d_lo + dspan - d);     // + i*RW: R(c-d) | R(c-d-1)<<8
+            uint32_t* csw = cs + wave * (kTileH * G::CSS) + lane;
+            uint32_t T = 0u, Tprev[2 * R + 1];
+            const bool m0 = (c >= 0) && (c < W) && (c >= d);
+            const bool m1 = (c >= 0) && (c < W) && (c >= d + 1);
+            if (!col_edge) {
+#pragma unroll
+                for (int i = 0; i < G::ROWS; ++i) {
+                    const uint32_t w = rcol[i * RW];
+                    T = __builtin_amdgcn_sad_u8((lp[i] & 0xFFu) | (w & 0xFF00u), w, T);
+                    T = __builtin_amdgcn_sad_hi_u8((w & 0xFFu) | (lp[i] & 0xFF00u), w, T);
+                    if (i >= 2 * R) {
+                        const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
+                        csw[(i - 2 * R) * G::CSS] = T - old;
+                    }
+                    Tprev[i % (2 * R + 1)] = T;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < G::ROWS; ++i) {
+                    const uint32_t w = rcol[i * RW];
+                    const uint32_t A = m0 ? ((lp[i] & 0xFFu) | (w & 0xFF00u)) : w;
+                    const uint32_t B = m1 ? ((w & 0xFFu) | (lp[i] & 0xFF00u)) : w;
+                    T = __builtin_amdgcn_sad_u8(A, w, T);
+                    T = __builtin_amdgcn_sad_hi_u8(B, w, T);
+                    if (i >= 2 * R) {
+                        const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
+                        csw[(i - 2 * R) * G::CSS] = T - old;
+                    }
+                    Tprev[i % (2 * R + 1)] = T;
+                }
+            }
+        }
+        __syncthreads();
+        // ================= phase H =================
+        {
+            const uint32_t* row = cs + wave * (kTileH * G::CSS) + hj * G::CSS + obase;
+            uint32_t v[4 * G::NCS4];
+#pragma unroll
+            for (int q = 0; q < G::NCS4; ++q) {
+                const uint4 x4 = *reinterpret_cast<const uint4*>(row + 4 * q);
+                v[4 * q + 0] = x4.x; v[4 * q + 1] = x4.y; v[4 * q + 2] = x4.z; v[4 * q + 3] = x4.w;
+            }
+            const uint32_t dsel = (uint32_t)(d & 0xFF) | ((uint32_t)((d + 1) & 0xFF) << 8);
+            uint32_t S = 0u;
+#pragma unroll
+            for (int k = 0; k < 2 * R; ++k) S += v[k];
+            const bool dm = d_edge || (d0 + kChunk > d_hi);
+            if (!dm) {
+#pragma unroll
+                for (int o = 0; o < G::NOUT; ++o) {
+                    S += v[o + 2 * R];
+                    const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                    const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                    best[o] = min(best[o], min(klo, khi));
+                    S -= v[o];
+                }
+            } else {
+#pragma unroll
+                for (int o = 0; o < G::NOUT; ++o) {
+                    S += v[o + 2 * R];
+                    const int x = x0 + obase + o;
+                    const int lim = a.valid_mode == 0 ? (W - x) : x;
+                    uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                    uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                    klo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
+                    khi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
+                    best[o] = min(best[o], min(klo, khi));
+                    S -= v[o];
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- fold the 4 pair-waves: best[w][j][o] through LDS, then min + store ----
+    {
+        uint32_t* bw = cs + wave * (kTileH * G::CSS) + hj * G::CSS + obase;
+#pragma unroll
+        for (int o = 0; o < G::NOUT; ++o) bw[o] = best[o];
+    }
+    __syncthreads();
+    uint8_t* Df = a.disp ? a.disp + (int64_t)frame * a.out_frame_stride : nullptr;
+    uint32_t* Kf = a.keys ? a.keys + (int64_t)frame * W * H : nullptr;
+    for (int e = tid; e < kTileH * G::TW; e += kThreads) {
+        const int j = e / G::TW, o = e - j * G::TW;
+        const int y = y0 + j, x = x0 + o;
+        if (y >= H || x >= W) continue;
+        const uint32_t* p = cs + j * G::CSS + o;
+        const uint32_t k = min(min(p[0], p[kTileH * G::CSS]), min(p[2 * kTileH * G::CSS], p[3 * kTileH * G::CSS]));
+        if (Df) Df[(int64_t)y * a.out_pitch + x] = k < a.thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
+        if (Kf) Kf[(int64_t)y * W + x] = k;
+    }
+}
+
+template <int R>
+hipError_t launch_r(const MatchArgs& a, int batch, hipStream_t s) {
+    using G = Geo<R>;
+    const int tiles_x = (a.W + G::TW - 1) / G::TW;
+    const int tiles_y = (a.H + kTileH - 1) / kTileH;
+    const size_t rs_bytes = (size_t)G::ROWS * (kCols + kMaxDisp) * 2;
+    const size_t lds = (size_t)G::CS_BYTES + ((rs_bytes + 15) & ~(size_t)15);
+    const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
+    if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(box_match_kernel<R>, dim3((unsigned)blocks), dim3(kThreads), lds, s, a, tiles_x, tiles_y);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Generic path for radius > 7 (u16 packing would overflow): direct window sum per (pixel, d)
+// straight from the reference formulation.  Correct for any radius; not a performance path.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void box_match_generic_kernel(MatchArgs a, int64_t total) {
+    const int64_t P = (int64_t)a.W * a.H;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const int frame = (int)(gid / P);
+    const int64_t p = gid - (int64_t)frame * P;
+    const int y = (int)(p / a.W), x = (int)(p - (int64_t)y * a.W);
+    const uint8_t* Lf = a.left + (int64_t)frame * a.frame_stride;
+    const uint8_t* Rf = a.right + (int64_t)frame * a.frame_stride;
+    const int r = a.radius;
+    uint32_t best = a.seed_key;
+    for (int d = a.d_lo; d < a.d_hi; ++d) {
+        const int lim = a.valid_mode == 0 ? (a.W - x) : x;
+        if (d > lim) continue;
+        uint32_t sad = 0;
+        for (int i = -r; i <= r; ++i) {
+            const int yy = y + i;
+            if (yy < 0 || yy >= a.H) continue;
+            const uint8_t* lr = Lf + (int64_t)yy * a.pitch;
+            const uint8_t* rr = Rf + (int64_t)yy * a.pitch;
+            for (int j = -r; j <= r; ++j) {
+                const int cc = x + j;
+                if (cc < 0 || cc >= a.W || cc < d) continue;
+                const int v = (int)lr[cc] - (int)rr[cc - d];
+                sad += (uint32_t)(v < 0 ? -v : v);
+            }
+        }
+        const uint32_t k = (sad << 8) | (uint32_t)(d & 0xFF);
+        best = k < best ? k : best;
+    }
+    if (a.disp) a.disp[(int64_t)frame * a.out_frame_stride + (int64_t)y * a.out_pitch + x] =
+        best < a.thresh_key ? (uint8_t)(best & 0xFFu) : (uint8_t)0;
+    if (a.keys) a.keys[(int64_t)frame * P + p] = best;
+}
+
+}  // namespace
+
+hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s) {
+    switch (a.radius) {
+        case 0: return launch_r<0>(a, batch, s);
+        case 1: return launch_r<1>(a, batch, s);
+        case 2: return launch_r<2>(a, batch, s);
+        case 3: return launch_r<3>(a, batch, s);
+        case 4: return launch_r<4>(a, batch, s);
+        case 5: return launch_r<5>(a, batch, s);
+        case 6: return launch_r<6>(a, batch, s);
+        case 7: return launch_r<7>(a, batch, s);
+        default: return launch_box_match_generic(a, batch, s);
+    }
+}
+
+hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s) {
+    const int64_t total = (int64_t)a.W * a.H * batch;
+    const int64_t blocks = (total + 255) / 256;
+    if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(box_match_generic_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, total);
+    return hipGetLastError();
+}
+
+}  // namespace sm

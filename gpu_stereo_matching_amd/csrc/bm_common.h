@@ -1,0 +1,41 @@
+// bm_common.h — shared definitions for the gfx950 block-matching kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sm {
+
+// Launch parameters of one block-matching pass over a batch of frames.
+struct MatchArgs {
+    const uint8_t* left;    // [batch][H][pitch]
+    const uint8_t* right;
+    int W, H, pitch;
+    int64_t frame_stride;   // bytes between frames (inputs)
+    int radius;             // window = (2r+1)^2 (SADWindowSize, Device.cu:181)
+    int d_lo, d_hi;         // disparities handled by this launch: [d_lo, d_hi)
+    int valid_mode;         // 0: d <= W - x (Device.cu:44);  1: d <= x (right view, mirrored)
+    uint32_t seed_key;      // starting best key: (50*win^2) << 8 (Device.cu:37) or ~0u (no threshold)
+    uint32_t thresh_key;    // disparity = key < thresh_key ? key & 0xFF : 0   (Device.cu:38,63)
+    uint8_t* disp;          // optional: uint8 disparity [batch][H][out_pitch]
+    int out_pitch;
+    int64_t out_frame_stride;
+    uint32_t* keys;         // optional: packed keys [batch][H][W] (multi-GPU slice reduction)
+};
+
+constexpr int kMaxDisp = 256;      // uint8 output / 8-bit d field of the packed key
+constexpr int kMaxFastRadius = 7;  // u16 packed sums stay < 2^16 up to r = 7 (15*15*255 = 57375)
+
+// Host-side launchers (bm_box.hip, bm_aux.hip).
+hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s);
+hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s);
+hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key,
+                               uint8_t* disp, int out_pitch, hipStream_t s);
+hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch,
+                         uint8_t* dst, int dst_pitch, int64_t dst_stride, hipStream_t s);
+hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride,
+                           const uint8_t* right_disp_mirrored, int rpitch, int64_t rstride,
+                           int W, int H, int batch, uint8_t* out, int opitch, int64_t ostride,
+                           uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
+                           hipStream_t s);
+
+}  // namespace sm

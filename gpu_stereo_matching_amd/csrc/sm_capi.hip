@@ -1,0 +1,360 @@
+// sm_capi.hip — the C ABI (include/sm_hip.h): handles, buffers, streams, entry points.
+//
+// Replaces blockMatching_gpu (BlockMatching/Device.cu:173-301).  Differences from the
+// reference that are deliberate and documented in DESIGN.md:
+//   * buffers are allocated once per handle, not per call, and are freed (Device.cu leaks
+//     ~2*P*D bytes and the output buffer per call, :185-194, :300);
+//   * every HIP call is checked and surfaced as an int status + sm_last_error_string()
+//     (the reference never checks, so its W > 1024 launch failure returns all zeros, :253);
+//   * any frame size works (the reference's fixed (8,10,D)x(32,32) grid covers 320x256 only, :231-233).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <cstdarg>
+#include <new>
+
+#include "../../include/sm_hip.h"
+#include "bm_common.h"
+#include "bm_guided.h"
+
+struct sm_handle {
+    int device = 0;
+    int max_w = 0, max_h = 0, max_d = 0;
+    hipStream_t stream = nullptr;
+    // frame buffers (one frame; batched device calls use caller memory)
+    uint8_t* d_left = nullptr;
+    uint8_t* d_right = nullptr;
+    uint8_t* d_disp = nullptr;
+    // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
+    uint8_t* d_lr = nullptr;
+    size_t lr_bytes = 0;
+    // guided workspace
+    sm::GuidedWorkspace gws;
+    float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float stage_ms[3] = {0.f, 0.f, 0.f};
+};
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define SM_HIP(call)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? SM_ERR_OUT_OF_MEMORY : SM_ERR_LAUNCH,      \
+                        "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+int check_geometry(const sm_handle* h, int width, int height, int pitch, int radius, int num_disp) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (width <= 0 || height <= 0) return fail(SM_ERR_INVALID_ARG, "bad frame size %dx%d", width, height);
+    if (pitch < width) return fail(SM_ERR_INVALID_ARG, "pitch %d < width %d", pitch, width);
+    if (radius < 0 || radius > 127) return fail(SM_ERR_INVALID_ARG, "radius %d out of [0,127]", radius);
+    if (num_disp < 1 || num_disp > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "num_disp %d out of [1,%d] (uint8 disparity output)", num_disp, sm::kMaxDisp);
+    const int64_t win = 2 * radius + 1;
+    if (((int64_t)50 * win * win) >= (int64_t)1 << 23)
+        return fail(SM_ERR_INVALID_ARG, "radius %d too large for the 32-bit (SAD<<8|d) key", radius);
+    return SM_OK;
+}
+
+uint32_t seed_key(int radius) {
+    const uint32_t win = 2u * (uint32_t)radius + 1u;
+    return (50u * win * win) << 8;  // Device.cu:37 start value, d field 0
+}
+
+int ensure_lr(sm_handle* h, size_t bytes) {
+    if (h->lr_bytes >= bytes) return SM_OK;
+    if (h->d_lr) (void)hipFree(h->d_lr);
+    h->d_lr = nullptr;
+    h->lr_bytes = 0;
+    SM_HIP(hipMalloc(&h->d_lr, bytes));
+    h->lr_bytes = bytes;
+    return SM_OK;
+}
+
+// Core device-side pass over `batch` frames.
+int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+               int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
+               uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
+    const bool guided = (flags & SM_AGG_GUIDED) != 0;
+    const bool lr = (flags & SM_LR_CHECK) != 0 || right_out || mask_out;
+    if (guided) {
+        if (lr) {
+            // guided + LR: right view by mirroring, same as the box path below
+            const int64_t P = (int64_t)W * H;
+            int rc = ensure_lr(h, (size_t)(3 * P * batch));
+            if (rc) return rc;
+            uint8_t* mL = h->d_lr;
+            uint8_t* mR = mL + P * batch;
+            uint8_t* rdm = mR + P * batch;
+            SM_HIP(sm::launch_guided_match(h->gws, L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0,
+                                          disp, opitch, ostride, s));
+            SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
+            SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
+            SM_HIP(sm::launch_guided_match(h->gws, mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, rdm, W,
+                                          P, s));
+            SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rdm, W, P, W, H, batch, disp, opitch, ostride,
+                                       right_out, mask_out, apitch, astride, s));
+            return SM_OK;
+        }
+        SM_HIP(sm::launch_guided_match(h->gws, L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, disp,
+                                      opitch, ostride, s));
+        return SM_OK;
+    }
+    sm::MatchArgs a{};
+    a.left = L;
+    a.right = R;
+    a.W = W;
+    a.H = H;
+    a.pitch = pitch;
+    a.frame_stride = fstride;
+    a.radius = radius;
+    a.d_lo = 0;
+    a.d_hi = D;
+    a.valid_mode = 0;
+    a.seed_key = seed_key(radius);
+    a.thresh_key = seed_key(radius);
+    a.disp = disp;
+    a.out_pitch = opitch;
+    a.out_frame_stride = ostride;
+    a.keys = nullptr;
+    SM_HIP(sm::launch_box_match(a, batch, s));
+    if (!lr) return SM_OK;
+
+    // Right view (StereoHelper.cpp:156-180 + :131-154) as the left matcher on the mirrored pair,
+    // validity d <= x (mirrored) and no threshold; then the StereoDisparity.cpp:136-147 check.
+    const int64_t P = (int64_t)W * H;
+    int rc = ensure_lr(h, (size_t)(3 * P * batch));
+    if (rc) return rc;
+    uint8_t* mL = h->d_lr;
+    uint8_t* mR = mL + P * batch;
+    uint8_t* rdm = mR + P * batch;
+    SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
+    SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
+    sm::MatchArgs b = a;
+    b.left = mL;
+    b.right = mR;
+    b.pitch = W;
+    b.frame_stride = P;
+    b.valid_mode = 1;
+    b.seed_key = 0xFFFFFFFFu;
+    b.thresh_key = 0xFFFFFFFFu;
+    b.disp = rdm;
+    b.out_pitch = W;
+    b.out_frame_stride = P;
+    SM_HIP(sm::launch_box_match(b, batch, s));
+    SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rdm, W, P, W, H, batch, disp, opitch, ostride, right_out,
+                               mask_out, apitch, astride, s));
+    return SM_OK;
+}
+
+int host_match(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+               int radius, int num_disp, unsigned flags, uint8_t* disp_out, uint8_t* right_out, uint8_t* mask_out,
+               int out_pitch) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (out_pitch < width) return fail(SM_ERR_INVALID_ARG, "out_pitch %d < width %d", out_pitch, width);
+    if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity %dx%d/D=%d", width, height, num_disp,
+                    h->max_w, h->max_h, h->max_d);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const int64_t P = (int64_t)width * height;
+    uint8_t* aux = nullptr;
+    if (right_out || mask_out) {
+        rc = ensure_lr(h, (size_t)(5 * P));  // 3P for the LR pass + 2P for right/mask outputs
+        if (rc) return rc;
+    }
+    SM_HIP(hipEventRecord(h->ev[0], s));
+    SM_HIP(hipMemcpy2DAsync(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipMemcpy2DAsync(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipEventRecord(h->ev[1], s));
+    if (right_out || mask_out) aux = h->d_lr + 3 * P;
+    rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
+                    right_out ? aux : nullptr, mask_out ? aux + P : nullptr, width, P, s);
+    if (rc) return rc;
+    SM_HIP(hipEventRecord(h->ev[2], s));
+    SM_HIP(hipMemcpy2DAsync(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
+    if (right_out) SM_HIP(hipMemcpy2DAsync(right_out, out_pitch, aux, width, width, height, hipMemcpyDeviceToHost, s));
+    if (mask_out) SM_HIP(hipMemcpy2DAsync(mask_out, out_pitch, aux + P, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipEventRecord(h->ev[3], s));
+    SM_HIP(hipEventSynchronize(h->ev[3]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    return SM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+SM_API const char* sm_version(void) { return "gpu_stereo_matching_amd 0.1.0 (gfx950)"; }
+
+SM_API const char* sm_last_error_string(void) { return g_err; }
+
+SM_API int sm_device_count(int* count) {
+    if (!count) return fail(SM_ERR_INVALID_ARG, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return SM_OK;
+}
+
+SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm_handle** out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    if (max_width <= 0 || max_height <= 0 || max_disp < 1 || max_disp > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "bad capacity %dx%d/D=%d", max_width, max_height, max_disp);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SM_ERR_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(SM_ERR_DEVICE, "device %d out of range (%d visible)", device, n);
+    hipDeviceProp_t prop;
+    SM_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SM_ERR_DEVICE, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+    SM_HIP(hipSetDevice(device));
+    sm_handle* h = new (std::nothrow) sm_handle();
+    if (!h) return fail(SM_ERR_OUT_OF_MEMORY, "host alloc");
+    h->device = device;
+    h->max_w = max_width;
+    h->max_h = max_height;
+    h->max_d = max_disp;
+    const size_t P = (size_t)max_width * max_height;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&h->d_left, P);
+    if (e == hipSuccess) e = hipMalloc(&h->d_right, P);
+    if (e == hipSuccess) e = hipMalloc(&h->d_disp, P);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
+    if (e != hipSuccess) {
+        sm_destroy(h);
+        return fail(e == hipErrorOutOfMemory ? SM_ERR_OUT_OF_MEMORY : SM_ERR_DEVICE, "sm_create: %s",
+                    hipGetErrorString(e));
+    }
+    *out = h;
+    return SM_OK;
+}
+
+SM_API int sm_destroy(sm_handle* h) {
+    if (!h) return SM_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(h->d_left);
+    (void)hipFree(h->d_right);
+    (void)hipFree(h->d_disp);
+    (void)hipFree(h->d_lr);
+    sm::guided_workspace_free(h->gws);
+    for (auto& ev : h->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return SM_OK;
+}
+
+SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (param == SM_PARAM_GUIDED_EPS) {
+        if (!(value > 0.f)) return fail(SM_ERR_INVALID_ARG, "guided eps must be > 0");
+        h->guided_eps = value;
+        return SM_OK;
+    }
+    return fail(SM_ERR_INVALID_ARG, "unknown param %d", param);
+}
+
+SM_API int sm_block_match_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                             int pitch, int radius, int num_disp, unsigned flags, uint8_t* disp_out, int out_pitch) {
+    return host_match(h, left, right, width, height, pitch, radius, num_disp, flags, disp_out, nullptr, nullptr,
+                      out_pitch);
+}
+
+SM_API int sm_block_match_lr_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                                int pitch, int radius, int num_disp, unsigned flags, uint8_t* disp_out,
+                                uint8_t* right_disp_out, uint8_t* valid_mask_out, int out_pitch) {
+    return host_match(h, left, right, width, height, pitch, radius, num_disp, flags | SM_LR_CHECK, disp_out,
+                      right_disp_out, valid_mask_out, out_pitch);
+}
+
+SM_API int sm_last_stage_ms(sm_handle* h, float* upload_ms, float* match_ms, float* download_ms) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (upload_ms) *upload_ms = h->stage_ms[0];
+    if (match_ms) *match_ms = h->stage_ms[1];
+    if (download_ms) *download_ms = h->stage_ms[2];
+    return SM_OK;
+}
+
+SM_API int sm_match_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                           int pitch, int batch, int64_t frame_stride, int radius, int num_disp, unsigned flags,
+                           uint8_t* d_disp, int out_pitch, int64_t out_frame_stride, void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!d_left || !d_right || !d_disp) return fail(SM_ERR_INVALID_ARG, "null device pointer");
+    if (batch < 1) return fail(SM_ERR_INVALID_ARG, "batch %d < 1", batch);
+    if (out_pitch < width) return fail(SM_ERR_INVALID_ARG, "out_pitch < width");
+    if (batch > 1 && (frame_stride < (int64_t)pitch * height || out_frame_stride < (int64_t)out_pitch * height))
+        return fail(SM_ERR_INVALID_ARG, "frame strides overlap");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    return run_device(h, d_left, d_right, width, height, pitch, batch, frame_stride, radius, num_disp, flags, d_disp,
+                      out_pitch, out_frame_stride, nullptr, nullptr, width, (int64_t)width * height, s);
+}
+
+SM_API int sm_slice_keys_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                                int pitch, int radius, int d_lo, int d_hi, uint32_t* d_keys, void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, d_hi > 0 ? d_hi : 1);
+    if (rc) return rc;
+    if (d_lo < 0 || d_hi <= d_lo || d_hi > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "bad slice [%d,%d)", d_lo, d_hi);
+    if (!d_left || !d_right || !d_keys) return fail(SM_ERR_INVALID_ARG, "null device pointer");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    sm::MatchArgs a{};
+    a.left = d_left;
+    a.right = d_right;
+    a.W = width;
+    a.H = height;
+    a.pitch = pitch;
+    a.frame_stride = (int64_t)pitch * height;
+    a.radius = radius;
+    a.d_lo = d_lo;
+    a.d_hi = d_hi;
+    a.valid_mode = 0;
+    a.seed_key = seed_key(radius);
+    a.thresh_key = seed_key(radius);
+    a.disp = nullptr;
+    a.keys = d_keys;
+    SM_HIP(sm::launch_box_match(a, 1, s));
+    return SM_OK;
+}
+
+SM_API int sm_keys_to_disp_device(sm_handle* h, const uint32_t* d_keys, int width, int height, int radius,
+                                  uint8_t* d_disp, int out_pitch, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_keys || !d_disp || width <= 0 || height <= 0 || out_pitch < width || radius < 0)
+        return fail(SM_ERR_INVALID_ARG, "bad keys_to_disp arguments");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    SM_HIP(sm::launch_keys_to_disp(d_keys, width, height, seed_key(radius), d_disp, out_pitch, s));
+    return SM_OK;
+}
+
+SM_API int sm_stream_sync(sm_handle* h, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return SM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+/*
+ * sm_hip.h — C ABI of the MI355X stereo block-matching engine (libsm_hip.so).
+ *
+ * Drop-in boundary for the reference's GPU proxy
+ *     void blockMatching_gpu(cv::Mat &h_left, cv::Mat &h_right, cv::Mat &h_disparity,
+ *                            int SADWindowSize, int searchRange);
+ * declared at BlockMatching/Device.cuh:50 and defined at BlockMatching/Device.cu:173-301.
+ * The reference's argument meaning is kept exactly:
+ *   SADWindowSize  -> `radius`    (window is (2*radius+1)^2; Device.cu:181, BlockMatching.cpp:119)
+ *   searchRange    -> `num_disp`  (disparities d = 0 .. num_disp-1; Device.cu:43)
+ * and so is the output convention: uint8 disparity, 0 where no window SAD falls
+ * below 50*win^2 (Device.cu:37-38,63).
+ *
+ * Everything is plain C: pointers, sizes, int status codes.  No OpenCV or torch
+ * types cross this boundary.  include/stereo_bm.hpp maps the reference's Mat API
+ * onto it; gpu_stereo_matching_amd/_capi.py binds it with ctypes.
+ *
+ * Threading: one handle per host thread.  A handle owns its device buffers,
+ * pinned staging and a HIP stream; calls on one handle are serialised.
+ */
+#ifndef SM_HIP_H
+#define SM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SM_API __attribute__((visibility("default")))
+
+/* ---- status codes (the reference has none: Device.cu never checks errors) ---- */
+enum {
+    SM_OK = 0,
+    SM_ERR_INVALID_ARG = 1,   /* bad size / pointer / radius / num_disp */
+    SM_ERR_OUT_OF_MEMORY = 2, /* hipMalloc / hipHostMalloc failed */
+    SM_ERR_DEVICE = 3,        /* no usable gfx950 device */
+    SM_ERR_LAUNCH = 4,        /* kernel launch or runtime error */
+    SM_ERR_CAPACITY = 5       /* frame larger than the handle was created for */
+};
+
+/* ---- aggregation / post-processing flags ---- */
+enum {
+    SM_AGG_BOX = 0u,        /* (2r+1)^2 zero-padded SAD window: the reference's kernalFindCorr */
+    SM_AGG_GUIDED = 1u,     /* guided-filter aggregation of the AD volume (this build's extension) */
+    SM_LR_CHECK = 2u        /* left-right consistency (STMatching/StereoDisparity.cpp:136-147):
+                               occluded pixels are written as 0 */
+};
+
+/* ---- scalar parameters (sm_set_param_f) ---- */
+enum {
+    SM_PARAM_GUIDED_EPS = 1 /* guided-filter epsilon in AD^2 units (default 6.5025 = 1e-4 * 255^2) */
+};
+
+typedef struct sm_handle sm_handle;
+
+/* Library / device information. */
+SM_API const char *sm_version(void);
+SM_API const char *sm_last_error_string(void);      /* thread-local message of the last failure */
+SM_API int sm_device_count(int *count);
+
+/* Create a handle on HIP device `device`, sized for frames up to max_width x max_height and
+ * up to max_disp disparities (1..256).  Device buffers and pinned staging are allocated once
+ * here (the reference re-allocates and leaks ~2*P*D bytes per call: Device.cu:185-194). */
+SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm_handle **out);
+SM_API int sm_destroy(sm_handle *h);
+SM_API int sm_set_param_f(sm_handle *h, int param, float value);
+
+/* Host-pointer entry point — the blockMatching_gpu replacement.
+ * left/right: uint8 gray, `height` rows of `width` bytes at row stride `pitch` (>= width).
+ * disp_out: uint8, `height` rows at stride `out_pitch`.  Synchronous, like the reference.
+ * flags: SM_AGG_BOX | SM_AGG_GUIDED, optionally | SM_LR_CHECK. */
+SM_API int sm_block_match_u8(sm_handle *h, const uint8_t *left, const uint8_t *right,
+                             int width, int height, int pitch, int radius, int num_disp,
+                             unsigned flags, uint8_t *disp_out, int out_pitch);
+
+/* Same, also returning the right-view disparity (may be NULL) and the LR valid mask
+ * (1 = consistent, may be NULL).  Implies SM_LR_CHECK. */
+SM_API int sm_block_match_lr_u8(sm_handle *h, const uint8_t *left, const uint8_t *right,
+                                int width, int height, int pitch, int radius, int num_disp,
+                                unsigned flags, uint8_t *disp_out, uint8_t *right_disp_out,
+                                uint8_t *valid_mask_out, int out_pitch);
+
+/* Per-stage timings of the last sm_block_match_* call in ms (hipEvents), mirroring the
+ * reference's "upload data / pre calculation / find corr / download data" printouts
+ * (Device.cu:218,238,257,292).  Any pointer may be NULL. */
+SM_API int sm_last_stage_ms(sm_handle *h, float *upload_ms, float *match_ms, float *download_ms);
+
+/* ---- device-pointer entry points (inputs already resident in HBM) ----
+ * All pointers are device pointers on the handle's device; `stream` is a hipStream_t used as
+ * given (NULL = the device's default stream, as in the HIP runtime API).  Asynchronous: nothing
+ * waits for completion.
+ * `batch` frames are stored back to back: frame i starts at ptr + i*frame_stride. */
+SM_API int sm_match_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right,
+                           int width, int height, int pitch, int batch, int64_t frame_stride,
+                           int radius, int num_disp, unsigned flags,
+                           uint8_t *d_disp, int out_pitch, int64_t out_frame_stride, void *stream);
+
+/* Disparity-slice keys for multi-GPU sharding over d: for every pixel the
+ * minimum over valid d in [d_lo, d_hi) of ((SAD << 8) | d), seeded with (50*win^2) << 8.
+ * Keys of disjoint slices combine with an elementwise unsigned min (an all-reduce MIN). */
+SM_API int sm_slice_keys_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right,
+                                int width, int height, int pitch, int radius, int d_lo, int d_hi,
+                                uint32_t *d_keys, void *stream);
+
+/* Key map -> disparity: d where (key >> 8) < 50*win^2, else 0 (Device.cu:37,57,63). */
+SM_API int sm_keys_to_disp_device(sm_handle *h, const uint32_t *d_keys, int width, int height,
+                                  int radius, uint8_t *d_disp, int out_pitch, void *stream);
+
+/* Async host<->device helpers on the handle's stream (pinned staging is internal). */
+SM_API int sm_stream_sync(sm_handle *h, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SM_HIP_H */

@@ -1,0 +1,453 @@
+/*
+ * bm_oracle.c — CPU restatement of the reference block-matching path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (gpu_stereo_matching_amd/,
+ * include/) links, loads or calls this file.  It is imported exclusively by
+ * tests/, by __graft_entry__.smoke() as the checker, and by bench.py's
+ * cpu_baseline leg (timed, never used to produce the measured GPU result).
+ *
+ * Reference: ningw42/GPU_Stereo_Matching (read-only at /root/reference).
+ * The reference's own CPU file BlockMatching/BlockMatching.cpp needs OpenCV
+ * headers that this image does not have, so it is unbuildable here (see
+ * DESIGN.md §Oracle).  Every function below restates the algorithm of the
+ * cited reference lines in plain C; the comments say which line each rule
+ * comes from.
+ *
+ * Layouts: images are uint8 row-major, width W, height H, row pitch == W.
+ *          cost volumes are d-major planes [D][H][W] (as Device.cu:193).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#define ORA_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------- */
+/* a9: gray conversion used by the caller before the path                    */
+/* Caller.cpp:15-16 cvtColor(..., CV_BGR2GRAY) on an imread() BGR image.     */
+/* OpenCV 2.4 8-bit fixed point: Y = (1868 B + 9617 G + 4899 R + 8192) >> 14  */
+/* ------------------------------------------------------------------------- */
+ORA_API void ora_bgr_to_gray(const uint8_t *bgr, int64_t npix, int channels, uint8_t *gray)
+{
+    for (int64_t i = 0; i < npix; ++i) {
+        const uint8_t *px = bgr + i * channels;
+        uint32_t y = 1868u * px[0] + 9617u * px[1] + 4899u * px[2] + 8192u;
+        gray[i] = (uint8_t)(y >> 14);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* a1: absolute-difference volume.                                           */
+/* PreCal BlockMatching.cpp:89-109 / kernalPreCal_V2 Device.cu:19-32:        */
+/*   dif[d][p] = |L[p] - R[p-d]| when (p mod W) >= d, else left at the       */
+/*   memset value 0 (BlockMatching.cpp:143, Device.cu:194).                  */
+/* ------------------------------------------------------------------------- */
+ORA_API void ora_precal(const uint8_t *L, const uint8_t *R, int W, int H, int D, uint8_t *dif)
+{
+    const int64_t P = (int64_t)W * H;
+    memset(dif, 0, (size_t)(P * D));
+    for (int d = 0; d < D; ++d) {
+        uint8_t *plane = dif + (int64_t)d * P;
+        for (int y = 0; y < H; ++y) {
+            const uint8_t *l = L + (int64_t)y * W;
+            const uint8_t *r = R + (int64_t)y * W;
+            uint8_t *o = plane + (int64_t)y * W;
+            for (int x = d; x < W; ++x) {
+                int v = (int)l[x] - (int)r[x - d];
+                o[x] = (uint8_t)(v < 0 ? -v : v);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* a2/a4: literal restatement of getDisp (BlockMatching.cpp:111-189), the    */
+/* CPU twin of kernalFindCorr (Device.cu:34-64).  Same loop nest, same       */
+/* early exit (:174-176), same start value 50*win^2 (:157), same -256 seed   */
+/* (:158) truncated to uchar on store (:184).  Used as the CPU baseline      */
+/* ("port") and as the slow-path checker.                                     */
+/*   dif: caller-provided scratch of P*D bytes, or NULL to allocate.          */
+/* ------------------------------------------------------------------------- */
+ORA_API int ora_get_disp(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                         uint8_t *out, uint8_t *dif)
+{
+    const int64_t P = (int64_t)W * H;
+    const int win = 2 * radius + 1;
+    const int taps = win * win;
+    uint8_t *own = NULL;
+    if (!dif) {
+        own = (uint8_t *)malloc((size_t)(P * D));
+        if (!own) return -1;
+        dif = own;
+    }
+    /* tap table: (dx, dy, linear offset) in raster order of the window
+       (BlockMatching.cpp:130-133: i%win - r, i/win - r, dx + dy*W) */
+    int *tdx = (int *)malloc(sizeof(int) * taps);
+    int *tdy = (int *)malloc(sizeof(int) * taps);
+    int64_t *toff = (int64_t *)malloc(sizeof(int64_t) * taps);
+    for (int t = 0; t < taps; ++t) {
+        tdx[t] = t % win - radius;
+        tdy[t] = t / win - radius;
+        toff[t] = tdx[t] + (int64_t)tdy[t] * W;
+    }
+    ora_precal(L, R, W, H, D, dif);
+
+    for (int64_t p = 0; p < P; ++p) {
+        const int col = (int)(p % W), row = (int)(p / W);
+        int best = 50 * taps;
+        int dm = -256;
+        for (int d = 0; d < D; ++d) {
+            if (col + d > W) break;                         /* :166 */
+            const uint8_t *plane = dif + (int64_t)d * P;
+            int acc = 0;
+            for (int t = 0; t < taps; ++t) {
+                int c = col + tdx[t];
+                if (c >= W || c < 0) continue;              /* :170 */
+                int rr = row + tdy[t];
+                if (rr >= H || rr < 0) continue;            /* :172 */
+                acc += plane[p + toff[t]];
+                if (acc > best) break;                      /* :174-176 */
+            }
+            if (acc < best) { best = acc; dm = d; }         /* :178-181 */
+        }
+        out[p] = (uint8_t)dm;                               /* :184 */
+    }
+    free(tdx); free(tdy); free(toff); free(own);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* a3: independent restatement of the same map as                            */
+/*   zero-padded (2r+1)^2 box sum of each AD plane                           */
+/*   + validity d <= W - x (the break at BlockMatching.cpp:166/Device.cu:44) */
+/*   + strict-< WTA seeded with 50*win^2, no match -> 0.                     */
+/* Separable running sums, O(P*D); fast enough for 1080p parity tests.       */
+/* Optional outputs: cost volume [D][H][W] int32 (box SAD, no validity), and */
+/* the winning packed key per pixel ((cost << 8) | d, or T << 8 for none).   */
+/* ------------------------------------------------------------------------- */
+static void box_plane(const uint8_t *L, const uint8_t *R, int W, int H, int r, int d,
+                      int32_t *colsum /* W */, int32_t *out /* H*W */)
+{
+    /* running vertical window sums per column (rows outside the image add
+       nothing), then a running horizontal window sum per row */
+    memset(colsum, 0, sizeof(int32_t) * W);
+    for (int yy = 0; yy < r && yy < H; ++yy) {
+        const uint8_t *l = L + (int64_t)yy * W, *rr = R + (int64_t)yy * W;
+        for (int x = d; x < W; ++x) { int v = (int)l[x] - (int)rr[x - d]; colsum[x] += v < 0 ? -v : v; }
+    }
+    for (int y = 0; y < H; ++y) {
+        if (y + r < H) {
+            const uint8_t *l = L + (int64_t)(y + r) * W, *rr = R + (int64_t)(y + r) * W;
+            for (int x = d; x < W; ++x) { int v = (int)l[x] - (int)rr[x - d]; colsum[x] += v < 0 ? -v : v; }
+        }
+        if (y - r - 1 >= 0) {
+            const uint8_t *l = L + (int64_t)(y - r - 1) * W, *rr = R + (int64_t)(y - r - 1) * W;
+            for (int x = d; x < W; ++x) { int v = (int)l[x] - (int)rr[x - d]; colsum[x] -= v < 0 ? -v : v; }
+        }
+        int32_t *o = out + (int64_t)y * W;
+        int32_t run = 0;
+        for (int x = 0; x < r && x < W; ++x) run += colsum[x];
+        for (int x = 0; x < W; ++x) {
+            if (x + r < W) run += colsum[x + r];
+            if (x - r - 1 >= 0) run -= colsum[x - r - 1];
+            o[x] = run;
+        }
+    }
+}
+
+ORA_API int ora_box_disp(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                         uint8_t *out, int32_t *cost_out, uint32_t *key_out)
+{
+    const int64_t P = (int64_t)W * H;
+    const int win = 2 * radius + 1;
+    const int32_t T = 50 * win * win;
+    int32_t *colsum = (int32_t *)malloc(sizeof(int32_t) * W);
+    int32_t *plane = (int32_t *)malloc(sizeof(int32_t) * P);
+    int32_t *best = (int32_t *)malloc(sizeof(int32_t) * P);
+    int32_t *bd = (int32_t *)malloc(sizeof(int32_t) * P);
+    if (!colsum || !plane || !best || !bd) { free(colsum); free(plane); free(best); free(bd); return -1; }
+    for (int64_t p = 0; p < P; ++p) { best[p] = T; bd[p] = -256; }
+    for (int d = 0; d < D; ++d) {
+        box_plane(L, R, W, H, radius, d, colsum, plane);
+        if (cost_out) memcpy(cost_out + (int64_t)d * P, plane, sizeof(int32_t) * P);
+        for (int y = 0; y < H; ++y) {
+            for (int x = 0; x < W; ++x) {
+                if (x + d > W) continue;
+                int64_t p = (int64_t)y * W + x;
+                if (plane[p] < best[p]) { best[p] = plane[p]; bd[p] = d; }
+            }
+        }
+    }
+    for (int64_t p = 0; p < P; ++p) {
+        out[p] = (uint8_t)bd[p];
+        if (key_out) key_out[p] = bd[p] < 0 ? ((uint32_t)T << 8) : (((uint32_t)best[p] << 8) | (uint32_t)(bd[p] & 0xFF));
+    }
+    free(colsum); free(plane); free(best); free(bd);
+    return 0;
+}
+
+/* Box SAD cost volume only ([D][H][W] int32), for LR / key tests. */
+ORA_API int ora_box_cost(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D, int32_t *cost)
+{
+    int32_t *colsum = (int32_t *)malloc(sizeof(int32_t) * W);
+    if (!colsum) return -1;
+    for (int d = 0; d < D; ++d)
+        box_plane(L, R, W, H, radius, d, colsum, cost + (int64_t)d * W * H);
+    free(colsum);
+    return 0;
+}
+
+/* Partial-range key map for one d-slice [d_lo, d_hi): per pixel the minimum of
+   (cost << 8 | d) over valid d in the slice, seeded with T << 8.  The min over
+   slices equals ora_box_disp's key (the multi-GPU reduction contract). */
+ORA_API int ora_box_keys_slice(const uint8_t *L, const uint8_t *R, int W, int H, int radius,
+                               int d_lo, int d_hi, uint32_t *keys)
+{
+    const int64_t P = (int64_t)W * H;
+    const int win = 2 * radius + 1;
+    const uint32_t seed = (uint32_t)(50 * win * win) << 8;
+    int32_t *colsum = (int32_t *)malloc(sizeof(int32_t) * W);
+    int32_t *plane = (int32_t *)malloc(sizeof(int32_t) * P);
+    if (!colsum || !plane) { free(colsum); free(plane); return -1; }
+    for (int64_t p = 0; p < P; ++p) keys[p] = seed;
+    for (int d = d_lo; d < d_hi; ++d) {
+        box_plane(L, R, W, H, radius, d, colsum, plane);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                if (x + d > W) continue;
+                int64_t p = (int64_t)y * W + x;
+                uint32_t k = ((uint32_t)plane[p] << 8) | (uint32_t)(d & 0xFF);
+                if (k < keys[p]) keys[p] = k;
+            }
+    }
+    free(colsum); free(plane);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* a7: left-right consistency.                                               */
+/* Right cost from the left volume, GetRightMatchingCostFromLeft             */
+/*   (STMatching/StereoHelper.cpp:156-180): C_R(y,x,d) = C_L(y,x+d,d) when   */
+/*   x+d < W, else C_R(y,x,d-1).                                             */
+/* Right WTA, GetDisparity_WTA (StereoHelper.cpp:131-154): argmin from d=0,  */
+/*   strict <, no threshold.                                                 */
+/* Check, StereoDisparity.cpp:136-147: d = dL(y,x); occluded when x-d < 0,   */
+/*   d == 0, or |d - dR(y,x-d)| > 1.  Output: checked map (occluded -> 0)    */
+/*   and the valid mask (!occ).                                              */
+/* cost: [D][H][W] int32 (ora_box_cost).                                     */
+/* ------------------------------------------------------------------------- */
+ORA_API void ora_right_wta(const int32_t *cost, int W, int H, int D, uint8_t *right_disp)
+{
+    const int64_t P = (int64_t)W * H;
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            int64_t rowbase = (int64_t)y * W;
+            /* walk d keeping the clamped value like StereoHelper.cpp:170-175 */
+            int32_t cur = cost[rowbase + x];              /* d = 0: x+0 < W */
+            int32_t minv = cur;
+            int minpos = 0;
+            for (int d = 1; d < D; ++d) {
+                if (x + d < W) cur = cost[(int64_t)d * P + rowbase + x + d];
+                /* else cur stays = C_R(y,x,d-1) */
+                if (cur < minv) { minv = cur; minpos = d; }
+            }
+            right_disp[rowbase + x] = (uint8_t)minpos;
+        }
+    }
+}
+
+ORA_API void ora_lr_check(const uint8_t *left_disp, const uint8_t *right_disp, int W, int H,
+                          uint8_t *checked, uint8_t *valid_mask)
+{
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            int64_t p = (int64_t)y * W + x;
+            int d = left_disp[p];
+            int occ;
+            if (x - d >= 0) {
+                int dr = right_disp[p - d];
+                int diff = d - dr;
+                occ = (d == 0) || (diff > 1 || diff < -1);
+            } else {
+                occ = 1;
+            }
+            if (checked) checked[p] = occ ? 0 : (uint8_t)d;
+            if (valid_mask) valid_mask[p] = (uint8_t)!occ;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* a8: guided-filter cost aggregation (absent from the reference; this       */
+/* build's definition, see DESIGN.md §Guided.  PARITY UNPINNED vs the        */
+/* reference, pinned only against this fp64 restatement.)                    */
+/*   guide I = L (0..255), cost p_d = AD_d (0..255, AD_d = 0 for x < d as a1),*/
+/*   f(.) = mean over the clipped (2r+1)^2 window (divide by in-image count), */
+/*   a = (f(I p) - f(I) f(p)) / (f(I I) - f(I)^2 + eps), b = f(p) - a f(I),   */
+/*   q = f(a) I + f(b);  WTA: seed 50.0 (= 50*win^2 / win^2), strict <,       */
+/*   validity d <= W - x, no match -> 0 (same rules as a2).                   */
+/* q_out (optional): [D][H][W] doubles.                                       */
+/* ------------------------------------------------------------------------- */
+static void box_mean_d(const double *src, int W, int H, int r, double *tmp, double *dst)
+{
+    /* vertical sums */
+    for (int x = 0; x < W; ++x) {
+        double run = 0.0;
+        for (int y = 0; y < r && y < H; ++y) run += src[(int64_t)y * W + x];
+        for (int y = 0; y < H; ++y) {
+            if (y + r < H) run += src[(int64_t)(y + r) * W + x];
+            if (y - r - 1 >= 0) run -= src[(int64_t)(y - r - 1) * W + x];
+            tmp[(int64_t)y * W + x] = run;
+        }
+    }
+    for (int y = 0; y < H; ++y) {
+        int ny = (y + r < H ? y + r : H - 1) - (y - r > 0 ? y - r : 0) + 1;
+        double run = 0.0;
+        const double *t = tmp + (int64_t)y * W;
+        for (int x = 0; x < r && x < W; ++x) run += t[x];
+        for (int x = 0; x < W; ++x) {
+            if (x + r < W) run += t[x + r];
+            if (x - r - 1 >= 0) run -= t[x - r - 1];
+            int nx = (x + r < W ? x + r : W - 1) - (x - r > 0 ? x - r : 0) + 1;
+            dst[(int64_t)y * W + x] = run / (double)(nx * ny);
+        }
+    }
+}
+
+/* Exact box sum of an integer plane, then divided by count: avoids running-sum
+   drift so the restatement is exact up to the final division. */
+static void box_mean_i(const int64_t *src, int W, int H, int r, int64_t *tmp, double *dst)
+{
+    for (int x = 0; x < W; ++x) {
+        int64_t run = 0;
+        for (int y = 0; y < r && y < H; ++y) run += src[(int64_t)y * W + x];
+        for (int y = 0; y < H; ++y) {
+            if (y + r < H) run += src[(int64_t)(y + r) * W + x];
+            if (y - r - 1 >= 0) run -= src[(int64_t)(y - r - 1) * W + x];
+            tmp[(int64_t)y * W + x] = run;
+        }
+    }
+    for (int y = 0; y < H; ++y) {
+        int ny = (y + r < H ? y + r : H - 1) - (y - r > 0 ? y - r : 0) + 1;
+        int64_t run = 0;
+        const int64_t *t = tmp + (int64_t)y * W;
+        for (int x = 0; x < r && x < W; ++x) run += t[x];
+        for (int x = 0; x < W; ++x) {
+            if (x + r < W) run += t[x + r];
+            if (x - r - 1 >= 0) run -= t[x - r - 1];
+            int nx = (x + r < W ? x + r : W - 1) - (x - r > 0 ? x - r : 0) + 1;
+            dst[(int64_t)y * W + x] = (double)run / (double)(nx * ny);
+        }
+    }
+}
+
+/* Box-mean helper shared with the tests: exact mean over the clipped window.
+   Double version of the f(.) above (vertical-then-horizontal order). */
+ORA_API void ora_box_mean_f64(const double *src, int W, int H, int r, double *dst)
+{
+    double *tmp = (double *)malloc(sizeof(double) * (size_t)W * H);
+    box_mean_d(src, W, H, r, tmp, dst);
+    free(tmp);
+}
+
+ORA_API int ora_guided_disp(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                            double eps, uint8_t *out, double *q_out, double *best_out)
+{
+    const int64_t P = (int64_t)W * H;
+    int64_t *isrc = (int64_t *)malloc(sizeof(int64_t) * P);
+    int64_t *itmp = (int64_t *)malloc(sizeof(int64_t) * P);
+    double *mI = (double *)malloc(sizeof(double) * P);
+    double *mII = (double *)malloc(sizeof(double) * P);
+    double *mp = (double *)malloc(sizeof(double) * P);
+    double *mIp = (double *)malloc(sizeof(double) * P);
+    double *a = (double *)malloc(sizeof(double) * P);
+    double *b = (double *)malloc(sizeof(double) * P);
+    double *ma = (double *)malloc(sizeof(double) * P);
+    double *mb = (double *)malloc(sizeof(double) * P);
+    double *dtmp = (double *)malloc(sizeof(double) * P);
+    double *best = (double *)malloc(sizeof(double) * P);
+    int *bd = (int *)malloc(sizeof(int) * P);
+    int rc = 0;
+    if (!isrc || !itmp || !mI || !mII || !mp || !mIp || !a || !b || !ma || !mb || !dtmp || !best || !bd) {
+        rc = -1;
+        goto done;
+    }
+
+    for (int64_t p = 0; p < P; ++p) isrc[p] = L[p];
+    box_mean_i(isrc, W, H, radius, itmp, mI);
+    for (int64_t p = 0; p < P; ++p) isrc[p] = (int64_t)L[p] * L[p];
+    box_mean_i(isrc, W, H, radius, itmp, mII);
+    for (int64_t p = 0; p < P; ++p) { best[p] = 50.0; bd[p] = -256; }
+
+    for (int d = 0; d < D; ++d) {
+        /* p_d = AD_d, with the a1 zero for x < d */
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                int64_t p = (int64_t)y * W + x;
+                int v = 0;
+                if (x >= d) { v = (int)L[p] - (int)R[p - d]; if (v < 0) v = -v; }
+                isrc[p] = v;
+            }
+        box_mean_i(isrc, W, H, radius, itmp, mp);
+        for (int64_t p = 0; p < P; ++p) isrc[p] *= L[p];
+        box_mean_i(isrc, W, H, radius, itmp, mIp);
+        for (int64_t p = 0; p < P; ++p) {
+            double var = mII[p] - mI[p] * mI[p];
+            double cov = mIp[p] - mI[p] * mp[p];
+            a[p] = cov / (var + eps);
+            b[p] = mp[p] - a[p] * mI[p];
+        }
+        box_mean_d(a, W, H, radius, dtmp, ma);
+        box_mean_d(b, W, H, radius, dtmp, mb);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                int64_t p = (int64_t)y * W + x;
+                double q = ma[p] * (double)L[p] + mb[p];
+                if (q_out) q_out[(int64_t)d * P + p] = q;
+                if (x + d > W) continue;
+                if (q < best[p]) { best[p] = q; bd[p] = d; }
+            }
+    }
+    for (int64_t p = 0; p < P; ++p) {
+        out[p] = (uint8_t)bd[p];
+        if (best_out) best_out[p] = best[p];
+    }
+done:
+    free(isrc); free(itmp); free(mI); free(mII); free(mp); free(mIp); free(a); free(b);
+    free(ma); free(mb); free(dtmp); free(best); free(bd);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic rectified pair: SplitMix64(seed) texture T of      */
+/* H x (W + 2D); L[y][x] = T[y][x + D], R[y][x] = T[y][x + D + gt(y)],       */
+/* gt(y) = 8 + floor(8y/H) * floor((D-16)/7) (clamped at >= 0 bands).         */
+/* Byte-for-byte the same as gpu_stereo_matching_amd.synth (numpy), which     */
+/* the tests check; kept here so the CPU baseline needs no numpy.             */
+/* ------------------------------------------------------------------------- */
+static uint64_t splitmix64_at(uint64_t seed, uint64_t i)
+{
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+ORA_API void ora_synth_pair(uint64_t seed, int W, int H, int D, uint8_t *L, uint8_t *R)
+{
+    const int TW = W + 2 * D;
+    int step = (D - 16) / 7;
+    if (step < 0) step = 0;
+    for (int y = 0; y < H; ++y) {
+        int gt = 8 + (8 * y / H) * step;
+        if (gt > D - 1) gt = D - 1;
+        if (gt < 0) gt = 0;
+        for (int x = 0; x < W; ++x) {
+            uint64_t iL = (uint64_t)y * TW + (uint64_t)(x + D);
+            uint64_t iR = (uint64_t)y * TW + (uint64_t)(x + D + gt);
+            L[(int64_t)y * W + x] = (uint8_t)(splitmix64_at(seed, iL) >> 56);
+            R[(int64_t)y * W + x] = (uint8_t)(splitmix64_at(seed, iR) >> 56);
+        }
+    }
+}
