@@ -1,0 +1,63 @@
+"""CPU tests: libsm_hip.so loads and exports every symbol include/sm_hip.h declares;
+calls that need no GPU behave."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "sm_hip.h")).read()
+    return sorted(set(re.findall(r"SM_API\s+[\w\s\*]+?\b(sm_\w+)\s*\(", txt)))
+
+
+def test_header_declares_expected_set():
+    from gpu_stereo_matching_amd import _capi
+    assert set(declared_symbols()) == set(_capi.EXPORTED)
+
+
+def test_library_exports_all_symbols():
+    from gpu_stereo_matching_amd import _capi
+    lib = _capi.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_version_and_errors_without_device():
+    from gpu_stereo_matching_amd import _capi
+    lib = _capi.load()
+    assert b"gfx950" in lib.sm_version()
+    n = ctypes.c_int(-1)
+    assert lib.sm_device_count(ctypes.byref(n)) == 0 and n.value >= 0
+    h = ctypes.c_void_p()
+    assert lib.sm_create(0, 0, 10, 64, ctypes.byref(h)) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_create(0, 64, 64, 300, ctypes.byref(h)) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_block_match_u8(None, None, None, 10, 10, 10, 1, 8, 0, None, 10) == _capi.SM_ERR_INVALID_ARG
+    assert b"null handle" in lib.sm_last_error_string()
+    if n.value == 0:
+        assert lib.sm_create(0, 64, 64, 64, ctypes.byref(h)) == _capi.SM_ERR_DEVICE
+
+
+def test_no_cpu_fallback_in_product():
+    """The product package must not import or load the oracle (test infrastructure only)."""
+    pkg = os.path.join(ROOT, "gpu_stereo_matching_amd")
+    bad = re.compile(r"^\s*(from\s+oracle|import\s+oracle)|libsm_oracle|ora_[a-z_]+\(", re.M)
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert not bad.search(txt), f
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from gpu_stereo_matching_amd import _capi
+    with pytest.raises(ImportError):
+        saved = _capi._lib
+        _capi._lib = None
+        try:
+            _capi.load(str(tmp_path / "nope.so"))
+        finally:
+            _capi._lib = saved

@@ -1,0 +1,208 @@
+"""GPU parity tests: the HIP path through the C ABI vs the oracle / golden fixtures.
+
+Integer SAD/WTA work is compared bit-exact.  Sizes: the bundled Middlebury
+pairs and the synthetic edge cases at their own size, 1080p and 4K synthetic pairs against the
+fast oracle formulation (ora_box_disp, O(P*D)).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sm():
+    import gpu_stereo_matching_amd as sm
+    return sm
+
+
+@pytest.fixture(scope="module")
+def matcher(sm):
+    m = sm.BlockMatcher(0, 3840, 2160, 256)
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def test_library_is_hip(sm):
+    assert "gfx950" in sm.version()
+
+
+def test_middlebury_golden_host_path(matcher, gray, bm_expected):
+    for k in bm_expected.files:
+        if k.startswith("lr/"):
+            continue
+        p, r, D = k.split("/")
+        got = matcher.match(gray[f"{p}/view1"], gray[f"{p}/view5"], int(r[1:]), int(D[1:]))
+        assert np.array_equal(got, bm_expected[k]), f"{k}: {int((got != bm_expected[k]).sum())} px differ"
+
+
+def test_reference_entry_point(sm, gray, bm_expected):
+    """blockMatching_gpu(g1, g2, 5, 64) as called at Caller.cpp:19."""
+    got = sm.blockMatching_gpu(gray["Art_/view1"], gray["Art_/view5"], 5, 64)
+    assert np.array_equal(got, bm_expected["Art_/r5/D64"])
+
+
+def test_synthetic_edge_cases(matcher, synth_expected):
+    names = sorted({f.split("/")[0] for f in synth_expected.files})
+    for n in names:
+        _, W, H, r, D = (int(v) for v in synth_expected[f"{n}/meta"])
+        got = matcher.match(synth_expected[f"{n}/L"], synth_expected[f"{n}/R"], r, D)
+        assert np.array_equal(got, synth_expected[f"{n}/disp"]), n
+
+
+@pytest.mark.parametrize("r", list(range(0, 10)))
+def test_every_radius(matcher, oracle, r):
+    rng = np.random.default_rng(100 + r)
+    H, W, D = 45, 150, 40
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = np.roll(L, -7, axis=1) ^ rng.integers(0, 8, (H, W), dtype=np.uint8)
+    assert np.array_equal(matcher.match(L, R, r, D), oracle.box_disp(L, R, r, D))
+
+
+@pytest.mark.parametrize("D", [1, 2, 7, 8, 9, 15, 16, 17, 63, 64, 65, 100, 127, 128, 129, 200, 255, 256])
+def test_every_disparity_count(matcher, oracle, D):
+    L, R = oracle.synth_pair(D, 301, 37, max(D, 16))
+    assert np.array_equal(matcher.match(L, R, 3, D), oracle.box_disp(L, R, 3, D))
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 50), (50, 1), (3, 3), (10, 200), (63, 31), (64, 32), (65, 33),
+                                 (127, 9), (513, 67)])
+def test_ragged_and_tiny_frames(matcher, oracle, W, H):
+    rng = np.random.default_rng(W * 1000 + H)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    for r, D in ((0, 5), (2, 64), (5, 256)):
+        assert np.array_equal(matcher.match(L, R, r, D), oracle.box_disp(L, R, r, D)), (r, D)
+
+
+def test_extreme_values(matcher, oracle):
+    """Saturated inputs: maximal window sums (255*win^2) must not wrap the packed u16 sums."""
+    H, W = 40, 120
+    for r in (5, 7):
+        L = np.zeros((H, W), np.uint8)
+        R = np.full((H, W), 255, np.uint8)
+        assert np.array_equal(matcher.match(L, R, r, 64), oracle.box_disp(L, R, r, 64))
+        L = np.full((H, W), 255, np.uint8)
+        R = np.zeros((H, W), np.uint8)
+        R[:, ::3] = 255
+        assert np.array_equal(matcher.match(L, R, r, 64), oracle.box_disp(L, R, r, 64))
+
+
+def test_pitched_host_input(sm, matcher, oracle, gray):
+    """Row pitch > width (a Mat ROI): the C ABI's `pitch` argument."""
+    import ctypes
+    L, R = gray["Art/view1"], gray["Art/view5"]
+    H, W = L.shape
+    P = W + 37
+    Lp = np.zeros((H, P), np.uint8)
+    Rp = np.zeros((H, P), np.uint8)
+    Lp[:, :W] = L
+    Rp[:, :W] = R
+    out = np.full((H, W + 5), 7, np.uint8)
+    rc = matcher._lib.sm_block_match_u8(matcher._h, Lp.ctypes.data, Rp.ctypes.data, W, H, P, 4, 64, 0,
+                                        out.ctypes.data, W + 5)
+    assert rc == 0
+    assert np.array_equal(out[:, :W], oracle.box_disp(L, R, 4, 64))
+    assert (out[:, W:] == 7).all()
+
+
+def test_device_path_batched(matcher, oracle, torch):
+    B, H, W, D, r = 3, 120, 333, 96, 4
+    pairs = [oracle.synth_pair(50 + i, W, H, D) for i in range(B)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for i in range(B):
+        assert np.array_equal(got[i], oracle.box_disp(pairs[i][0], pairs[i][1], r, D)), i
+
+
+def test_1080p_d128_synthetic(matcher, oracle, torch):
+    """The bench workload (cfg3 geometry) at full size."""
+    L, R = oracle.synth_pair(1234, 1920, 1080, 128)
+    want = oracle.box_disp(L, R, 5, 128)
+    out = matcher.match_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), 5, 128)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    # size-independent property: on the banded synthetic pair most pixels recover ground truth
+    from gpu_stereo_matching_amd.synth import ground_truth_rows
+    gt = ground_truth_rows(1080, 128)[:, None]
+    acc = (want[:, 200:] == gt).mean()
+    assert acc > 0.95
+
+
+def test_1080p_d256_and_4k_d192(matcher, oracle, torch):
+    for (W, H, D, seed) in ((1920, 1080, 256, 1234), (3840, 2160, 192, 4321)):
+        L, R = oracle.synth_pair(seed, W, H, D)
+        want = oracle.box_disp(L, R, 5, D)
+        out = matcher.match_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), 5, D)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want), (W, H, D)
+
+
+def test_lr_golden(matcher, gray, bm_expected):
+    for k in [k for k in bm_expected.files if k.startswith("lr/") and k.endswith("/checked")]:
+        _, p, r, D, _ = k.split("/")
+        chk, rd, mask = matcher.match_lr(gray[f"{p}/view1"], gray[f"{p}/view5"], int(r[1:]), int(D[1:]))
+        assert np.array_equal(rd, bm_expected[k.replace("checked", "right")]), k
+        assert np.array_equal(chk, bm_expected[k]), k
+        assert np.array_equal(mask, bm_expected[k.replace("checked", "mask")]), k
+        # the flag form returns the same checked map
+        chk2 = matcher.match(gray[f"{p}/view1"], gray[f"{p}/view5"], int(r[1:]), int(D[1:]), lr_check=True)
+        assert np.array_equal(chk2, chk)
+
+
+@pytest.mark.parametrize("r,D", [(1, 16), (4, 64), (5, 128)])
+def test_lr_random(matcher, oracle, r, D):
+    L, R = oracle.synth_pair(r * 7 + D, 257, 61, max(D, 16))
+    disp, rd, chk, mask = oracle.box_lr(L, R, r, D)
+    c, rr, mm = matcher.match_lr(L, R, r, D)
+    assert np.array_equal(rr, rd) and np.array_equal(c, chk) and np.array_equal(mm, mask)
+
+
+@pytest.mark.parametrize("cuts", [[0, 128], [0, 64, 128], [0, 16, 32, 48, 64, 80, 96, 112, 128], [0, 5, 77, 128]])
+def test_slice_keys_min_equals_full(matcher, oracle, torch, cuts):
+    """The multi-GPU d-slice contract on one device: MIN over slice key maps == single pass."""
+    L, R = oracle.synth_pair(77, 400, 90, 128)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    disp, keys = oracle.box_disp(L, R, 5, 128, want_keys=True)
+    parts = [matcher.slice_keys_device(Lt, Rt, 5, a, b) for a, b in zip(cuts[:-1], cuts[1:])]
+    k = parts[0].clone()
+    for p in parts[1:]:
+        k = torch.minimum(k, p)
+    torch.cuda.synchronize()
+    assert np.array_equal(k.cpu().numpy().view(np.uint32), keys)
+    for (a, b), p in zip(zip(cuts[:-1], cuts[1:]), parts):
+        assert np.array_equal(p.cpu().numpy().view(np.uint32), oracle.box_keys_slice(L, R, 5, a, b)), (a, b)
+    d = matcher.keys_to_disp_device(k, 5)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), disp)
+
+
+def test_error_codes(sm, matcher):
+    L = np.zeros((10, 10), np.uint8)
+    with pytest.raises(sm.SMError) as e:
+        matcher.match(L, L, 1, 0)
+    assert e.value.code == 1
+    with pytest.raises(sm.SMError) as e:
+        matcher.match(L, L, 1, 257)
+    assert e.value.code == 1
+    small = sm.BlockMatcher(0, 16, 16, 32)
+    with pytest.raises(sm.SMError) as e:
+        small.match(np.zeros((17, 16), np.uint8), np.zeros((17, 16), np.uint8), 1, 8)
+    assert e.value.code == 5
+    small.close()
+
+
+def test_stage_timings(matcher, gray):
+    matcher.match(gray["Art_/view1"], gray["Art_/view5"], 5, 64)
+    u, c, d = matcher.stage_ms()
+    assert u > 0 and c > 0 and d > 0

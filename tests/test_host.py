@@ -1,0 +1,51 @@
+"""CPU tests of host-side code: synthetic generator, gray conversion, API argument checks."""
+import numpy as np
+import pytest
+
+import gpu_stereo_matching_amd as sm
+from gpu_stereo_matching_amd.synth import ground_truth_rows
+
+
+@pytest.mark.parametrize("seed,W,H,D", [(1234, 97, 33, 128), (1, 50, 20, 8), (4321, 301, 70, 192)])
+def test_synth_matches_c_generator(oracle, seed, W, H, D):
+    a = sm.synth_pair(seed, W, H, D)
+    b = oracle.synth_pair(seed, W, H, D)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_synth_ground_truth_shift():
+    W, H, D = 200, 64, 128
+    L, R = sm.synth_pair(9, W, H, D)
+    gt = ground_truth_rows(H, D)
+    for y in range(H):
+        g = int(gt[y])
+        assert np.array_equal(R[y, : W - g], L[y, g:])
+
+
+def test_gray_formula_opencv24(oracle):
+    rng = np.random.default_rng(0)
+    bgr = rng.integers(0, 256, (17, 23, 3), dtype=np.uint8)
+    g = sm.bgr_to_gray(bgr)
+    assert np.array_equal(g, oracle.bgr_to_gray(bgr))
+    # fixed points of the fixed-point formula
+    assert sm.bgr_to_gray(np.full((1, 1, 3), 255, np.uint8))[0, 0] == 255
+    assert sm.bgr_to_gray(np.array([[[0, 0, 255]]], np.uint8))[0, 0] == (4899 * 255 + 8192) >> 14
+    bgra = np.concatenate([bgr, np.full((17, 23, 1), 9, np.uint8)], axis=2)
+    assert np.array_equal(sm.bgr_to_gray(bgra), g)
+
+
+def test_gray_fixtures_are_gray(gray):
+    assert gray["Art_/view1"].shape == (256, 320)
+    assert gray["Art/view1"].shape == (370, 463)
+    assert gray["Laundry/view1"].shape == (370, 447)
+    assert gray["Art_/view1"].dtype == np.uint8
+
+
+def test_api_rejects_bad_images():
+    with pytest.raises(ValueError):
+        sm._as_u8_image(np.zeros((4, 4), np.float32), "x")
+    with pytest.raises(ValueError):
+        sm._as_u8_image(np.zeros((4, 4, 3), np.uint8), "x")
+    with pytest.raises(ValueError):
+        sm._flags("median", False)
+    assert sm._flags("guided", True) == sm.SM_AGG_GUIDED | sm.SM_LR_CHECK

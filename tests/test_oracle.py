@@ -1,0 +1,132 @@
+"""CPU tests: the oracle (oracle/bm_oracle.c) against the committed golden vectors and
+against itself (two independent formulations), plus the host-side helpers."""
+import numpy as np
+import pytest
+
+
+def _cases(bm_expected):
+    for k in bm_expected.files:
+        if k.startswith("lr/"):
+            continue
+        p, r, D = k.split("/")
+        yield k, p, int(r[1:]), int(D[1:])
+
+
+def test_golden_middlebury_reproduced(oracle, gray, bm_expected):
+    """Stored expected maps (getDisp restatement at generation time) == oracle now, both forms."""
+    for k, p, r, D in _cases(bm_expected):
+        L, R = gray[f"{p}/view1"], gray[f"{p}/view5"]
+        fast = oracle.box_disp(L, R, r, D)
+        assert np.array_equal(fast, bm_expected[k]), k
+    # the literal loop nest (slow) on the singleFrame config (Caller.cpp:19) and cfg1
+    for k in ("Art_/r5/D64", "Art/r3/D64"):
+        p, r, D = k.split("/")
+        lit = oracle.get_disp(gray[f"{p}/view1"], gray[f"{p}/view5"], int(r[1:]), int(D[1:]))
+        assert np.array_equal(lit, bm_expected[k]), k
+
+
+def test_golden_synthetic_reproduced(oracle, synth_expected):
+    names = sorted({f.split("/")[0] for f in synth_expected.files})
+    assert len(names) >= 8
+    for n in names:
+        seed, W, H, r, D = (int(v) for v in synth_expected[f"{n}/meta"])
+        L, R = synth_expected[f"{n}/L"], synth_expected[f"{n}/R"]
+        if n != "flat":
+            gL, gR = oracle.synth_pair(seed, W, H, max(D, 16))
+            assert np.array_equal(gL, L) and np.array_equal(gR, R), n
+        assert np.array_equal(oracle.get_disp(L, R, r, D), synth_expected[f"{n}/disp"]), n
+
+
+def test_flat_images_all_zero(oracle):
+    """All-equal pair: every SAD is 0, d = 0 wins everywhere (strict <, Device.cu:57)."""
+    img = np.full((20, 33), 200, np.uint8)
+    assert (oracle.get_disp(img, img, 2, 16) == 0).all()
+
+
+def test_threshold_no_match_is_zero(oracle):
+    """Maximal-difference pair: no SAD < 50*win^2 -> dm stays -256 -> (uchar)0 (Device.cu:38,63)."""
+    L = np.zeros((16, 40), np.uint8)
+    R = np.full((16, 40), 255, np.uint8)
+    d = oracle.get_disp(L, R, 1, 8)
+    # only columns x < d have zero AD; x=0 can still match d>=1 windows partially -> compare forms
+    assert np.array_equal(d, oracle.box_disp(L, R, 1, 8))
+
+
+@pytest.mark.parametrize("shape,r,D", [((9, 7), 0, 1), ((13, 31), 2, 40), ((25, 18), 4, 64), ((6, 70), 3, 256)])
+def test_two_formulations_agree_random(oracle, shape, r, D):
+    rng = np.random.default_rng(hash((shape, r, D)) & 0xFFFF)
+    L = rng.integers(0, 256, shape, dtype=np.uint8)
+    R = rng.integers(0, 256, shape, dtype=np.uint8)
+    assert np.array_equal(oracle.get_disp(L, R, r, D), oracle.box_disp(L, R, r, D))
+
+
+def test_key_slices_combine_by_min(oracle, gray):
+    """Multi-GPU contract: min over d-slices of the packed keys == full-range key,
+    and the finalised disparity equals the single-device map."""
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    disp, keys = oracle.box_disp(L, R, 5, 64, want_keys=True)
+    for cuts in ([0, 64], [0, 16, 32, 48, 64], [0, 7, 9, 40, 64], [0, 1, 2, 3, 64]):
+        parts = [oracle.box_keys_slice(L, R, 5, a, b) for a, b in zip(cuts[:-1], cuts[1:])]
+        k = np.minimum.reduce(parts)
+        assert np.array_equal(k, keys), cuts
+        T = 50 * 11 * 11
+        d = np.where((k >> 8) < T, k & 0xFF, 0).astype(np.uint8)
+        assert np.array_equal(d, disp)
+
+
+def test_lr_golden(oracle, gray, bm_expected):
+    for k in [k for k in bm_expected.files if k.startswith("lr/") and k.endswith("/checked")]:
+        _, p, r, D, _ = k.split("/")
+        disp, rd, chk, mask = oracle.box_lr(gray[f"{p}/view1"], gray[f"{p}/view5"], int(r[1:]), int(D[1:]))
+        assert np.array_equal(rd, bm_expected[k.replace("checked", "right")])
+        assert np.array_equal(chk, bm_expected[k])
+        assert np.array_equal(mask, bm_expected[k.replace("checked", "mask")])
+        # properties of the StereoDisparity.cpp:136-147 rule
+        assert ((chk == 0) | (chk == disp)).all()
+        assert (chk[mask == 1] > 0).all()
+
+
+def test_lr_rule_by_hand(oracle):
+    """Tiny hand case of the occlusion rule: x-d<0 -> occluded, d==0 -> occluded, |d-dR|>1 -> occluded."""
+    dl = np.array([[0, 1, 2, 3, 1, 2]], np.uint8)
+    dr = np.array([[1, 1, 2, 0, 0, 4]], np.uint8)
+    chk, mask = oracle.lr_check(dl, dr)
+    # x=0 d=0 occ; x=1 d=1 -> dR(0)=1 ok; x=2 d=2 -> dR(0)=1 ok; x=3 d=3 -> dR(0)=1 occ;
+    # x=4 d=1 -> dR(3)=0 ok (|1-0|=1); x=5 d=2 -> dR(3)=0 occ
+    assert mask.tolist() == [[0, 1, 1, 0, 1, 0]]
+    assert chk.tolist() == [[0, 1, 2, 0, 1, 0]]
+
+
+def test_right_wta_clamp_rule(oracle):
+    """GetRightMatchingCostFromLeft clamp (StereoHelper.cpp:170-175): for x+d >= W the right cost
+    repeats C_R(x,d-1), which can never win a strict < — so dR(x) <= W-1-x."""
+    rng = np.random.default_rng(3)
+    L = rng.integers(0, 256, (12, 30), dtype=np.uint8)
+    R = rng.integers(0, 256, (12, 30), dtype=np.uint8)
+    cost = oracle.box_cost(L, R, 2, 24)
+    rd = oracle.right_wta(cost)
+    x = np.arange(30)[None, :]
+    assert (rd <= (29 - x)).all()
+
+
+def test_guided_golden(oracle, gray, guided_expected):
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    disp, best = oracle.guided_disp(L, R, 5, 64, 1e-4 * 255 * 255)
+    assert np.array_equal(disp, guided_expected["Art_/r5/D64/disp"])
+    np.testing.assert_allclose(best, guided_expected["Art_/r5/D64/best"], rtol=0, atol=1e-9)
+
+
+def test_guided_large_eps_tends_to_box_mean(oracle):
+    """eps -> inf: a -> 0, b -> mean(p), q -> mean(mean(p)) (a box-of-box filter)."""
+    rng = np.random.default_rng(5)
+    L = rng.integers(0, 256, (20, 24), dtype=np.uint8)
+    R = rng.integers(0, 256, (20, 24), dtype=np.uint8)
+    _, q, _ = oracle.guided_disp(L, R, 2, 4, 1e12, want_q=True)
+    for d in range(4):
+        ad = np.zeros((20, 24))
+        ad[:, d:] = np.abs(L[:, d:].astype(int) - R[:, :24 - d].astype(int))
+        m1 = np.empty_like(ad)
+        m2 = np.empty_like(ad)
+        oracle.lib().ora_box_mean_f64(ad.ctypes.data_as(oracle._f64p), 24, 20, 2, m1.ctypes.data_as(oracle._f64p))
+        oracle.lib().ora_box_mean_f64(m1.ctypes.data_as(oracle._f64p), 24, 20, 2, m2.ctypes.data_as(oracle._f64p))
+        np.testing.assert_allclose(q[d], m2, atol=1e-6)
