@@ -31,10 +31,11 @@ constexpr int kPairs = 4;
 constexpr int kChunk = 2 * kPairs;
 constexpr int kCols = 64;
 
-template <int R>
+template <int R, int DMAX>
 struct Geo {
     static constexpr int TW = kCols - 2 * R;                  // output columns per tile
     static constexpr int ROWS = kTileH + 2 * R;                 // input rows per tile
+    static constexpr int NLQ = (ROWS + 3) / 4;                  // packed-L dwords per lane
     static constexpr int NOUT = (((TW + 1) / 2) + 3) & ~3;      // outputs per phase-H thread
     static constexpr int NCS4 = (NOUT + 2 * R + 3) / 4;         // 16-B CS reads per phase-H thread
     static constexpr int NEED = (NOUT + 4 * NCS4) > kCols ? (NOUT + 4 * NCS4) : kCols;
@@ -42,18 +43,31 @@ struct Geo {
     // 16 distinct 4-bank slots (conflict-free)
     static constexpr int CSS = (NEED % 8 <= 4) ? NEED + (4 - NEED % 8) : NEED + (12 - NEED % 8);
     static constexpr int CS_BYTES = kPairs * kTileH * CSS * 4;
+    static constexpr int RW = kCols + DMAX;                     // u16 entries per right-band row
+    static constexpr int RS_BYTES = ((ROWS * RW * 2) + 15) & ~15;
+    static constexpr int LDS_BYTES = CS_BYTES + RS_BYTES;
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p, int y, int x, int W, int H, int pitch) {
     return (y >= 0 && y < H && x >= 0 && x < W) ? (uint32_t)p[(int64_t)y * pitch + x] : 0u;
 }
 
-template <int R>
-__global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
-    using G = Geo<R>;
+// v_perm_b32 selectors building the v_sad operands from w = R(c-d) | R(c-d-1) << 8 and the packed
+// left column word lq (L of rows 4q..4q+3 in bytes 0..3); pool byte 0-3 = lq, 4-7 = w:
+//   A = [L, R(c-d-1), 0, 0]  -> sad_u8(A, w)    = |L - R(c-d)|
+//   B = [R(c-d), L, 0, 0]    -> sad_hi_u8(B, w) = |L - R(c-d-1)| << 16
+// A masked lane (AD forced to 0: column outside the image or c < d) uses A = B = w.
+__host__ __device__ constexpr uint32_t sel_a(int k) { return 0x0C0C0500u | (uint32_t)k; }
+__host__ __device__ constexpr uint32_t sel_b(int k) { return 0x0C0C0004u | ((uint32_t)k << 8); }
+constexpr uint32_t kSelW = 0x0C0C0504u;
+
+template <int R, int DMAX>
+__global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
+    using G = Geo<R, DMAX>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [kPairs][kTileH][CSS]
     uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::CS_BYTES);       // [ROWS][RW]
+    uint8_t* rsb = smem + G::CS_BYTES;                                    // byte view of rs
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -73,22 +87,36 @@ __global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int
 
     const int d_lo = a.d_lo, d_hi = a.d_hi;
     const int dspan = (d_hi - d_lo + kChunk - 1) & ~(kChunk - 1);
-    constexpr int RW = kCols + kMaxDisp;           // u16 entries per R row in LDS (fixed: immediate offsets)
-    const int RWU = kCols + dspan;                 // entries actually staged per row
+    const int RWU = kCols + dspan;                 // entries staged per row (<= RW)
     const int base = x0 - R - d_lo - dspan;        // image column of rs[.][0]
 
-    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8 ----
-    for (int e = tid; e < G::ROWS * RWU; e += kThreads) {
-        const int i = e / RWU, k = e - i * RWU;
-        const int y = y0 - R + i, c = base + k;
-        const uint32_t v = ld_u8(Rf, y, c, W, H, a.pitch) | (ld_u8(Rf, y, c - 1, W, H, a.pitch) << 8);
-        rs[i * RW + k] = (uint16_t)v;
+    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8.
+    //      Each byte is loaded once (coalesced along the row) and written to its two slots. ----
+    for (int i = 0; i < G::ROWS; ++i) {
+        const int y = y0 - R + i;
+        const bool row_in = (y >= 0) && (y < H);
+        const uint8_t* src = Rf + (int64_t)(row_in ? y : 0) * a.pitch;
+        uint8_t* dst = rsb + i * (G::RW * 2);
+        for (int k = tid - 1; k < RWU; k += kThreads) {
+            const int c = base + k;
+            const uint8_t v = (row_in && c >= 0 && c < W) ? src[c] : (uint8_t)0;
+            if (k >= 0) dst[2 * k] = v;
+            if (k + 1 < RWU) dst[2 * (k + 1) + 1] = v;
+        }
     }
-    // ---- this lane's left column, L in bytes 0 and 1 (for the v_bfi operand build) ----
+    // ---- this lane's left column, packed 4 rows per dword ----
     const int c = x0 - R + lane;                   // image column of CS column `lane`
-    uint32_t lp[G::ROWS];
+    uint32_t lq[G::NLQ];
 #pragma unroll
-    for (int i = 0; i < G::ROWS; ++i) lp[i] = ld_u8(Lf, y0 - R + i, c, W, H, a.pitch) * 0x0101u;
+    for (int q = 0; q < G::NLQ; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = 4 * q + b;
+            if (i < G::ROWS) v |= ld_u8(Lf, y0 - R + i, c, W, H, a.pitch) << (8 * b);
+        }
+        lq[q] = v;
+    }
 
     // ---- per-thread phase-H state: (row j, half h) of pair `wave` ----
     const int hj = lane & 31;
@@ -98,9 +126,9 @@ __global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int
 #pragma unroll
     for (int o = 0; o < G::NOUT; ++o) best[o] = a.seed_key;
 
-    const bool col_edge = (x0 - R < 0) || (x0 - R + kCols > W) || (x0 - R < d_hi - 1);
     const int xmax_tile = min(x0 + G::TW, W) - 1;
     const bool d_edge = a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0);
+    const bool col_in = (c >= 0) && (c < W);
 
     __syncthreads();
 
@@ -110,35 +138,27 @@ __global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int
         {
             const uint16_t* rcol = rs + (lane + d_lo + dspan - d);     // + i*RW: R(c-d) | R(c-d-1)<<8
             uint32_t* csw = cs + wave * (kTileH * G::CSS) + lane;
+            const bool m0 = col_in && (c >= d);
+            const bool m1 = col_in && (c >= d + 1);
+            uint32_t sa[4], sb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                sa[k] = m0 ? sel_a(k) : kSelW;
+                sb[k] = m1 ? sel_b(k) : kSelW;
+            }
             uint32_t T = 0u, Tprev[2 * R + 1];
-            const bool m0 = (c >= 0) && (c < W) && (c >= d);
-            const bool m1 = (c >= 0) && (c < W) && (c >= d + 1);
-            if (!col_edge) {
 #pragma unroll
-                for (int i = 0; i < G::ROWS; ++i) {
-                    const uint32_t w = rcol[i * RW];
-                    T = __builtin_amdgcn_sad_u8((lp[i] & 0xFFu) | (w & 0xFF00u), w, T);
-                    T = __builtin_amdgcn_sad_hi_u8((w & 0xFFu) | (lp[i] & 0xFF00u), w, T);
-                    if (i >= 2 * R) {
-                        const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
-                        csw[(i - 2 * R) * G::CSS] = T - old;
-                    }
-                    Tprev[i % (2 * R + 1)] = T;
+            for (int i = 0; i < G::ROWS; ++i) {
+                const uint32_t w = rcol[i * G::RW];
+                const uint32_t A = __builtin_amdgcn_perm(w, lq[i >> 2], sa[i & 3]);
+                const uint32_t B = __builtin_amdgcn_perm(w, lq[i >> 2], sb[i & 3]);
+                T = __builtin_amdgcn_sad_u8(A, w, T);
+                T = __builtin_amdgcn_sad_hi_u8(B, w, T);
+                if (i >= 2 * R) {
+                    const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
+                    csw[(i - 2 * R) * G::CSS] = T - old;
                 }
-            } else {
-#pragma unroll
-                for (int i = 0; i < G::ROWS; ++i) {
-                    const uint32_t w = rcol[i * RW];
-                    const uint32_t A = m0 ? ((lp[i] & 0xFFu) | (w & 0xFF00u)) : w;
-                    const uint32_t B = m1 ? ((w & 0xFFu) | (lp[i] & 0xFF00u)) : w;
-                    T = __builtin_amdgcn_sad_u8(A, w, T);
-                    T = __builtin_amdgcn_sad_hi_u8(B, w, T);
-                    if (i >= 2 * R) {
-                        const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
-                        csw[(i - 2 * R) * G::CSS] = T - old;
-                    }
-                    Tprev[i % (2 * R + 1)] = T;
-                }
+                Tprev[i % (2 * R + 1)] = T;
             }
         }
         __syncthreads();
@@ -203,17 +223,24 @@ __global__ __launch_bounds__(kThreads, 2) void box_match_kernel(MatchArgs a, int
     }
 }
 
-template <int R>
-hipError_t launch_r(const MatchArgs& a, int batch, hipStream_t s) {
-    using G = Geo<R>;
+template <int R, int DMAX>
+hipError_t launch_rd(const MatchArgs& a, int batch, hipStream_t s) {
+    using G = Geo<R, DMAX>;
     const int tiles_x = (a.W + G::TW - 1) / G::TW;
     const int tiles_y = (a.H + kTileH - 1) / kTileH;
-    const size_t rs_bytes = (size_t)G::ROWS * (kCols + kMaxDisp) * 2;
-    const size_t lds = (size_t)G::CS_BYTES + ((rs_bytes + 15) & ~(size_t)15);
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(box_match_kernel<R>, dim3((unsigned)blocks), dim3(kThreads), lds, s, a, tiles_x, tiles_y);
+    hipLaunchKernelGGL((box_match_kernel<R, DMAX>), dim3((unsigned)blocks), dim3(kThreads), (size_t)G::LDS_BYTES, s,
+                       a, tiles_x, tiles_y);
     return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_r(const MatchArgs& a, int batch, hipStream_t s) {
+    const int dspan = (a.d_hi - a.d_lo + kChunk - 1) & ~(kChunk - 1);
+    if (dspan <= 64) return launch_rd<R, 64>(a, batch, s);
+    if (dspan <= 128) return launch_rd<R, 128>(a, batch, s);
+    return launch_rd<R, 256>(a, batch, s);
 }
 
 // ---------------------------------------------------------------------------------------

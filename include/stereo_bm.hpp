@@ -1,0 +1,140 @@
+// stereo_bm.hpp — header-only C++ adapter that keeps the reference's host API
+//   void blockMatching_gpu(Mat &h_left, Mat &h_right, Mat &h_disparity,
+//                          int SADWindowSize, int searchRange);          // Device.cuh:50
+// on top of the C ABI in sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame) shaped caller
+// compiles and runs unchanged apart from the include.
+//
+// Works with cv::Mat when OpenCV is available (define SM_WITH_OPENCV before including, after
+// including <opencv2/core/core.hpp>), and with the minimal sm::Mat below otherwise (this image
+// has no OpenCV).  Any Mat-like type with rows, cols, data, step and a create(rows, cols, type)
+// member, or sm::Mat's (rows, cols, CV_8UC1) constructor, is accepted.
+//
+// Behaviour vs the reference (Device.cu:173-301):
+//   same arguments, same disparity values (bit-exact), same stdout stage lines
+//   ("upload data : ms", "find corr : ms", "download data : ms") when SM_VERBOSE is set;
+//   the output Mat owns its memory (the reference wraps a leaked new[] buffer, :185/:300);
+//   errors are reported on std::cerr and leave an all-zero map, like the reference's silent
+//   launch failure but visible.
+#pragma once
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "sm_hip.h"
+
+#ifndef CV_8UC1
+#define CV_8UC1 0
+#endif
+
+namespace sm {
+
+// Minimal single-channel 8-bit image (the subset of cv::Mat that the reference's path uses).
+struct Mat {
+    int rows = 0, cols = 0;
+    size_t step = 0;                     // bytes per row
+    uint8_t* data = nullptr;
+    std::shared_ptr<std::vector<uint8_t>> store;
+
+    Mat() = default;
+    Mat(int r, int c, int type = CV_8UC1) { create(r, c, type); }
+    // wrap external memory (not owned), like cv::Mat(rows, cols, CV_8UC1, ptr)
+    Mat(int r, int c, int /*type*/, void* ptr, size_t stp = 0)
+        : rows(r), cols(c), step(stp ? stp : (size_t)c), data(static_cast<uint8_t*>(ptr)) {}
+    void create(int r, int c, int /*type*/ = CV_8UC1) {
+        if (r == rows && c == cols && store) return;
+        rows = r;
+        cols = c;
+        step = (size_t)c;
+        store = std::make_shared<std::vector<uint8_t>>((size_t)r * c, 0);
+        data = store->data();
+    }
+    template <typename T> T* ptr(int r = 0) { return reinterpret_cast<T*>(data + (size_t)r * step); }
+    template <typename T> const T* ptr(int r = 0) const { return reinterpret_cast<const T*>(data + (size_t)r * step); }
+    bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
+    size_t total() const { return (size_t)rows * cols; }
+};
+
+namespace detail {
+
+struct Engine {
+    sm_handle* h = nullptr;
+    int w = 0, hgt = 0, d = 0;
+    ~Engine() { if (h) sm_destroy(h); }
+    bool ensure(int width, int height, int ndisp) {
+        if (h && width <= w && height <= hgt && ndisp <= d) return true;
+        if (h) sm_destroy(h);
+        h = nullptr;
+        w = width > 1920 ? width : 1920;
+        hgt = height > 1080 ? height : 1080;
+        d = 256;
+        int dev = 0;
+        if (const char* e = std::getenv("SM_DEVICE")) dev = std::atoi(e);
+        if (sm_create(dev, w, hgt, d, &h) != SM_OK) {
+            std::cerr << "sm_create: " << sm_last_error_string() << std::endl;
+            h = nullptr;
+            return false;
+        }
+        return true;
+    }
+};
+
+inline Engine& engine() {
+    static thread_local Engine e;   // one handle per host thread (sm_hip.h threading contract)
+    return e;
+}
+
+template <typename M> inline size_t row_step(const M& m) { return (size_t)m.step; }
+
+template <typename M> inline void make_output(M& out, int rows, int cols) { out.create(rows, cols, CV_8UC1); }
+
+}  // namespace detail
+
+// Mat-agnostic implementation (cv::Mat or sm::Mat).
+template <typename M>
+inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int SADWindowSize, int searchRange,
+                          unsigned flags = SM_AGG_BOX) {
+    const int rows = h_left.rows, cols = h_left.cols;
+    detail::make_output(h_disparity, rows, cols);
+    if (h_right.rows != rows || h_right.cols != cols) {
+        std::cerr << "blockMatching_gpu: left/right sizes differ" << std::endl;
+        return SM_ERR_INVALID_ARG;
+    }
+    detail::Engine& e = detail::engine();
+    if (!e.ensure(cols, rows, searchRange)) return SM_ERR_DEVICE;
+    int rc = sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
+                               SADWindowSize, searchRange, flags, h_disparity.data,
+                               (int)detail::row_step(h_disparity));
+    if (rc != SM_OK) {
+        std::cerr << "blockMatching_gpu: " << sm_last_error_string() << std::endl;
+        for (int r = 0; r < rows; ++r) std::memset(h_disparity.data + (size_t)r * detail::row_step(h_disparity), 0, cols);
+        return rc;
+    }
+    if (std::getenv("SM_VERBOSE")) {
+        float up = 0, mt = 0, dn = 0;
+        sm_last_stage_ms(e.h, &up, &mt, &dn);
+        std::cout << "upload data : " << up << std::endl;        // Device.cu:218
+        std::cout << "find corr : " << mt << std::endl;          // Device.cu:257 (pre calculation fused)
+        std::cout << "download data : " << dn << std::endl;      // Device.cu:292
+    }
+    return rc;
+}
+
+}  // namespace sm
+
+// ---- the reference's free function, unchanged signature (Device.cuh:50) ----
+#ifdef SM_WITH_OPENCV
+inline void blockMatching_gpu(cv::Mat& h_left, cv::Mat& h_right, cv::Mat& h_disparity, int SADWindowSize,
+                              int searchRange) {
+    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange);
+}
+#else
+inline void blockMatching_gpu(sm::Mat& h_left, sm::Mat& h_right, sm::Mat& h_disparity, int SADWindowSize,
+                              int searchRange) {
+    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange);
+}
+#endif

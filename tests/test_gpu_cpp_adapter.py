@@ -1,0 +1,42 @@
+"""The C++ drop-in path: examples/Main.cpp -> singleFrame() -> blockMatching_gpu(Mat&...) ->
+C ABI -> HIP, compared with the golden map of Caller.cpp:19's configuration."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "examples", "build", "single_frame")
+
+
+def _write_pgm(path, a):
+    with open(path, "wb") as f:
+        f.write(b"P5\n%d %d\n255\n" % (a.shape[1], a.shape[0]))
+        f.write(np.ascontiguousarray(a).tobytes())
+
+
+def _read_pgm(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    w, h = (int(v) for v in parts[1].split())
+    return np.frombuffer(parts[3], np.uint8).reshape(h, w)
+
+
+def test_example_builds():
+    assert os.path.exists(EXE), "examples/build/single_frame missing: run __graft_entry__.build()"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pair,sad,rng", [("Art_", 5, 64), ("Books", 4, 64)])
+def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):
+    _write_pgm(tmp_path / "l.pgm", gray[f"{pair}/view1"])
+    _write_pgm(tmp_path / "r.pgm", gray[f"{pair}/view5"])
+    env = dict(os.environ, SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
+               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD=str(sad), SM_RANGE=str(rng), SM_VERBOSE="1")
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "GPU : " in r.stdout and "find corr : " in r.stdout
+    got = _read_pgm(tmp_path / "d.pgm")
+    assert np.array_equal(got, bm_expected[f"{pair}/r{sad}/D{rng}"])
