@@ -43,13 +43,32 @@ struct Geo {
     // 16 distinct 4-bank slots (conflict-free)
     static constexpr int CSS = (NEED % 8 <= 4) ? NEED + (4 - NEED % 8) : NEED + (12 - NEED % 8);
     static constexpr int CS_BYTES = kPairs * kTileH * CSS * 4;
-    static constexpr int RW = kCols + DMAX;                     // u16 entries per right-band row
+    static constexpr int RW = kCols + DMAX + 4;                 // u16 entries per right-band row (x4-aligned base)
+    static constexpr int NDW = RW / 4;                          // dwords staged per right-band row
+    static constexpr int LSTR = kCols + 4;                      // bytes per staged left row
     static constexpr int RS_BYTES = ((ROWS * RW * 2) + 15) & ~15;
     static constexpr int LDS_BYTES = CS_BYTES + RS_BYTES;
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p, int y, int x, int W, int H, int pitch) {
     return (y >= 0 && y < H && x >= 0 && x < W) ? (uint32_t)p[(int64_t)y * pitch + x] : 0u;
+}
+
+// 4 image bytes of row y from column x (little-endian), bytes outside the image read as 0.
+// Interior dwords are one (possibly unaligned) global_load_dword; border dwords go byte-wise.
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p, int y, int x, int W, int H, int pitch) {
+    if (y < 0 || y >= H) return 0u;
+    const uint8_t* row = p + (int64_t)y * pitch;
+    if (x >= 0 && x + 3 < W) {
+        uint32_t v;
+        __builtin_memcpy(&v, row + x, 4);
+        return v;
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        if (x + b >= 0 && x + b < W) v |= (uint32_t)row[x + b] << (8 * b);
+    return v;
 }
 
 // v_perm_b32 selectors building the v_sad operands from w = R(c-d) | R(c-d-1) << 8 and the packed
@@ -87,35 +106,51 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
 
     const int d_lo = a.d_lo, d_hi = a.d_hi;
     const int dspan = (d_hi - d_lo + kChunk - 1) & ~(kChunk - 1);
-    const int RWU = kCols + dspan;                 // entries staged per row (<= RW)
-    const int base = x0 - R - d_lo - dspan;        // image column of rs[.][0]
+    const int base = (x0 - R - d_lo - dspan) & ~3;   // image column of rs[.][0] (floor to x4)
+    const int off0 = x0 - R - base;                  // rs index of (column c = x0-R+lane) at d = 0, minus lane
 
-    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8.
-    //      Each byte is loaded once (coalesced along the row) and written to its two slots. ----
-    for (int i = 0; i < G::ROWS; ++i) {
-        const int y = y0 - R + i;
-        const bool row_in = (y >= 0) && (y < H);
-        const uint8_t* src = Rf + (int64_t)(row_in ? y : 0) * a.pitch;
-        uint8_t* dst = rsb + i * (G::RW * 2);
-        for (int k = tid - 1; k < RWU; k += kThreads) {
-            const int c = base + k;
-            const uint8_t v = (row_in && c >= 0 && c < W) ? src[c] : (uint8_t)0;
-            if (k >= 0) dst[2 * k] = v;
-            if (k + 1 < RWU) dst[2 * (k + 1) + 1] = v;
+    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8, from dword loads
+    //      (all issued before any LDS write; image borders read as 0) ----
+    {
+        constexpr int N = G::ROWS * G::NDW;
+#pragma unroll 4
+        for (int e = tid; e < N; e += kThreads) {
+            const int i = e / G::NDW, j = e - (e / G::NDW) * G::NDW;
+            const int y = y0 - R + i, col = base + 4 * j;
+            const uint32_t cur = ld_u32(Rf, y, col, W, H, a.pitch);
+            const uint32_t prv = ld_u32(Rf, y, col - 4, W, H, a.pitch);
+            uint2 v;
+            v.x = __builtin_amdgcn_perm(cur, prv, 0x04050304u);   // [b0, p3, b1, b0]
+            v.y = __builtin_amdgcn_perm(cur, cur, 0x06070506u);   // [b2, b1, b3, b2]
+            *reinterpret_cast<uint2*>(rs + i * G::RW + 4 * j) = v;
         }
     }
-    // ---- this lane's left column, packed 4 rows per dword ----
+    // ---- stage the left tile (64 columns from x0-R) into the CS area, then pack this lane's
+    //      column 4 rows per dword ----
     const int c = x0 - R + lane;                   // image column of CS column `lane`
-    uint32_t lq[G::NLQ];
-#pragma unroll
-    for (int q = 0; q < G::NLQ; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int i = 4 * q + b;
-            if (i < G::ROWS) v |= ld_u8(Lf, y0 - R + i, c, W, H, a.pitch) << (8 * b);
+    const int lbase = (x0 - R) & ~3;
+    {
+        uint8_t* ls = smem;                        // [ROWS][LSTR] bytes, aliases cs (unused yet)
+        constexpr int NL = G::ROWS * (G::LSTR / 4);
+        for (int e = tid; e < NL; e += kThreads) {
+            const int i = e / (G::LSTR / 4), j = e - (e / (G::LSTR / 4)) * (G::LSTR / 4);
+            *reinterpret_cast<uint32_t*>(ls + i * G::LSTR + 4 * j) = ld_u32(Lf, y0 - R + i, lbase + 4 * j, W, H, a.pitch);
         }
-        lq[q] = v;
+    }
+    __syncthreads();
+    uint32_t lq[G::NLQ];
+    {
+        const uint8_t* lcol = smem + (c - lbase);
+#pragma unroll
+        for (int q = 0; q < G::NLQ; ++q) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int i = 4 * q + b;
+                if (i < G::ROWS) v |= (uint32_t)lcol[i * G::LSTR] << (8 * b);
+            }
+            lq[q] = v;
+        }
     }
 
     // ---- per-thread phase-H state: (row j, half h) of pair `wave` ----
@@ -136,7 +171,7 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
         const int d = d0 + 2 * wave;               // this wave's pair: d, d+1
         // ================= phase V =================
         {
-            const uint16_t* rcol = rs + (lane + d_lo + dspan - d);     // + i*RW: R(c-d) | R(c-d-1)<<8
+            const uint16_t* rcol = rs + (lane + off0 - d);           // + i*RW: R(c-d) | R(c-d-1)<<8
             uint32_t* csw = cs + wave * (kTileH * G::CSS) + lane;
             const bool m0 = col_in && (c >= d);
             const bool m1 = col_in && (c >= d + 1);
