@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
         }
     }
 
-    // ---- per-thread phase-H state: (row j, half h) of pair `wave` ----
+    // ---- per-thread phase-H state: (row j, half h); the wave owns pairs [p_lo, p_hi) ----
     const int hj = lane & 31;
     const int hh = lane >> 5;
     const int obase = hh * G::NOUT;                // first tile output column of this thread
@@ -164,15 +164,19 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
     const int xmax_tile = min(x0 + G::TW, W) - 1;
     const bool d_edge = a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0);
     const bool col_in = (c >= 0) && (c < W);
+    const int npairs = dspan >> 1;                 // multiple of 4
+    const int p_lo = (wave * npairs) / 4;
+    const int p_hi = ((wave + 1) * npairs) / 4;
+    uint32_t* csw = cs + wave * (kTileH * G::CSS);   // this wave's private CS plane
 
-    __syncthreads();
+    __syncthreads();   // lq reads of the aliased staging area are done before any CS write
 
-    for (int d0 = d_lo; d0 < d_lo + dspan; d0 += kChunk) {
-        const int d = d0 + 2 * wave;               // this wave's pair: d, d+1
-        // ================= phase V =================
+    for (int p = p_lo; p < p_hi; ++p) {
+        const int d = d_lo + 2 * p;                // pair (d, d+1)
+        // ================= phase V (lane = CS column) =================
         {
             const uint16_t* rcol = rs + (lane + off0 - d);           // + i*RW: R(c-d) | R(c-d-1)<<8
-            uint32_t* csw = cs + wave * (kTileH * G::CSS) + lane;
+            uint32_t* col = csw + lane;
             const bool m0 = col_in && (c >= d);
             const bool m1 = col_in && (c >= d + 1);
             uint32_t sa[4], sb[4];
@@ -191,15 +195,19 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
                 T = __builtin_amdgcn_sad_hi_u8(B, w, T);
                 if (i >= 2 * R) {
                     const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
-                    csw[(i - 2 * R) * G::CSS] = T - old;
+                    col[(i - 2 * R) * G::CSS] = T - old;
                 }
                 Tprev[i % (2 * R + 1)] = T;
             }
         }
-        __syncthreads();
-        // ================= phase H =================
+        // the CS plane is private to this wave: LDS ops of one wave complete in order, so only
+        // the compiler must not move the phase-H reads above the phase-V writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ================= phase H (lane = row x half-row) =================
         {
-            const uint32_t* row = cs + wave * (kTileH * G::CSS) + hj * G::CSS + obase;
+            const uint32_t* row = csw + hj * G::CSS + obase;
             uint32_t v[4 * G::NCS4];
 #pragma unroll
             for (int q = 0; q < G::NCS4; ++q) {
@@ -210,7 +218,7 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
             uint32_t S = 0u;
 #pragma unroll
             for (int k = 0; k < 2 * R; ++k) S += v[k];
-            const bool dm = d_edge || (d0 + kChunk > d_hi);
+            const bool dm = d_edge || (d + 1 >= d_hi);
             if (!dm) {
 #pragma unroll
                 for (int o = 0; o < G::NOUT; ++o) {
@@ -235,8 +243,11 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
                 }
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    __syncthreads();
 
     // ---- fold the 4 pair-waves: best[w][j][o] through LDS, then min + store ----
     {
