@@ -35,19 +35,25 @@ template <int R, int DMAX>
 struct Geo {
     static constexpr int TW = kCols - 2 * R;                  // output columns per tile
     static constexpr int ROWS = kTileH + 2 * R;                 // input rows per tile
+    static constexpr int HALF = kTileH / 2;                     // rows per CS hand-off
     static constexpr int NLQ = (ROWS + 3) / 4;                  // packed-L dwords per lane
-    static constexpr int NOUT = (((TW + 1) / 2) + 3) & ~3;      // outputs per phase-H thread
-    static constexpr int NCS4 = (NOUT + 2 * R + 3) / 4;         // 16-B CS reads per phase-H thread
-    static constexpr int NEED = (NOUT + 4 * NCS4) > kCols ? (NOUT + 4 * NCS4) : kCols;
-    // row stride in dwords, == 4 (mod 8) so 16 rows read by one ds_read_b128 lane group hit
-    // 16 distinct 4-bank slots (conflict-free)
-    static constexpr int CSS = (NEED % 8 <= 4) ? NEED + (4 - NEED % 8) : NEED + (12 - NEED % 8);
-    static constexpr int CS_BYTES = kPairs * kTileH * CSS * 4;
+    static constexpr int NQ = (((TW + 3) / 4) + 1) & ~1;        // outputs per phase-H thread (even: b64 reads)
+    static constexpr int NCS2 = (NQ + 2 * R + 1) / 2;           // 8-B CS reads per phase-H thread
+    static constexpr int NEED = 3 * NQ + 2 * NCS2;              // last CS column read + 1
+    // row stride in dwords == 4 (mod 64): the 32 lanes of a ds_read_b64 group (16 rows x 2
+    // quarters, quarter offsets NQ apart with NQ == 2 mod 4) start on 32 distinct even banks
+    static constexpr int CSS = ((NEED - 4 + 63) / 64) * 64 + 4;
+    static constexpr int CS_BYTES = 4 * HALF * CSS * 4;         // 4 waves x one half-tile plane
     static constexpr int RW = kCols + DMAX + 4;                 // u16 entries per right-band row (x4-aligned base)
     static constexpr int NDW = RW / 4;                          // dwords staged per right-band row
     static constexpr int LSTR = kCols + 4;                      // bytes per staged left row
     static constexpr int RS_BYTES = ((ROWS * RW * 2) + 15) & ~15;
-    static constexpr int LDS_BYTES = CS_BYTES + RS_BYTES;
+    static constexpr int FOLD_BYTES = kTileH * TW * 4;          // final cross-wave fold plane
+    static constexpr int L_BYTES = ROWS * LSTR;                 // staged left tile
+    static constexpr int FRONT0 = CS_BYTES > FOLD_BYTES ? CS_BYTES : FOLD_BYTES;
+    static constexpr int FRONT = ((FRONT0 > L_BYTES ? FRONT0 : L_BYTES) + 15) & ~15;  // CS / fold / L alias
+    static constexpr int LDS_BYTES = FRONT + RS_BYTES;
+    static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p, int y, int x, int W, int H, int pitch) {
@@ -81,12 +87,12 @@ __host__ __device__ constexpr uint32_t sel_b(int k) { return 0x0C0C0004u | ((uin
 constexpr uint32_t kSelW = 0x0C0C0504u;
 
 template <int R, int DMAX>
-__global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
+__global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     using G = Geo<R, DMAX>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [kPairs][kTileH][CSS]
-    uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::CS_BYTES);       // [ROWS][RW]
-    uint8_t* rsb = smem + G::CS_BYTES;                                    // byte view of rs
+    uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::FRONT);          // [ROWS][RW]
+    uint8_t* rsb = smem + G::FRONT;                                       // byte view of rs
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -153,13 +159,15 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
         }
     }
 
-    // ---- per-thread phase-H state: (row j, half h); the wave owns pairs [p_lo, p_hi) ----
-    const int hj = lane & 31;
-    const int hh = lane >> 5;
-    const int obase = hh * G::NOUT;                // first tile output column of this thread
-    uint32_t best[G::NOUT];
+    // ---- per-thread phase-H state: (row j of the half, quarter q); the wave owns pairs [p_lo, p_hi) ----
+    const int hj = lane & 15;
+    const int hq = lane >> 4;
+    const int obase = hq * G::NQ;                  // first tile output column of this thread
+    uint32_t best[2][G::NQ];
 #pragma unroll
-    for (int o = 0; o < G::NOUT; ++o) best[o] = a.seed_key;
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int o = 0; o < G::NQ; ++o) best[h][o] = a.seed_key;
 
     const int xmax_tile = min(x0 + G::TW, W) - 1;
     const bool d_edge = a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0);
@@ -167,27 +175,30 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
     const int npairs = dspan >> 1;                 // multiple of 4
     const int p_lo = (wave * npairs) / 4;
     const int p_hi = ((wave + 1) * npairs) / 4;
-    uint32_t* csw = cs + wave * (kTileH * G::CSS);   // this wave's private CS plane
+    uint32_t* csw = cs + wave * (G::HALF * G::CSS);   // this wave's private half-tile CS plane
 
     __syncthreads();   // lq reads of the aliased staging area are done before any CS write
 
     for (int p = p_lo; p < p_hi; ++p) {
         const int d = d_lo + 2 * p;                // pair (d, d+1)
-        // ================= phase V (lane = CS column) =================
-        {
-            const uint16_t* rcol = rs + (lane + off0 - d);           // + i*RW: R(c-d) | R(c-d-1)<<8
-            uint32_t* col = csw + lane;
-            const bool m0 = col_in && (c >= d);
-            const bool m1 = col_in && (c >= d + 1);
-            uint32_t sa[4], sb[4];
+        const uint16_t* rcol = rs + (lane + off0 - d);               // + i*RW: R(c-d) | R(c-d-1)<<8
+        uint32_t* col = csw + lane;
+        const bool m0 = col_in && (c >= d);
+        const bool m1 = col_in && (c >= d + 1);
+        uint32_t sa[4], sb[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                sa[k] = m0 ? sel_a(k) : kSelW;
-                sb[k] = m1 ? sel_b(k) : kSelW;
-            }
-            uint32_t T = 0u, Tprev[2 * R + 1];
+        for (int k = 0; k < 4; ++k) {
+            sa[k] = m0 ? sel_a(k) : kSelW;
+            sb[k] = m1 ? sel_b(k) : kSelW;
+        }
+        const uint32_t dsel = (uint32_t)(d & 0xFF) | ((uint32_t)((d + 1) & 0xFF) << 8);
+        const bool dm = d_edge || (d + 1 >= d_hi);
+        uint32_t T = 0u, Tprev[2 * R + 1];
 #pragma unroll
-            for (int i = 0; i < G::ROWS; ++i) {
+        for (int h = 0; h < 2; ++h) {
+            // ====== phase V (lane = CS column): input rows of this half, CS rows h*HALF.. ======
+#pragma unroll
+            for (int i = (h == 0 ? 0 : 2 * R + G::HALF); i < (h == 0 ? 2 * R + G::HALF : G::ROWS); ++i) {
                 const uint32_t w = rcol[i * G::RW];
                 const uint32_t A = __builtin_amdgcn_perm(w, lq[i >> 2], sa[i & 3]);
                 const uint32_t B = __builtin_amdgcn_perm(w, lq[i >> 2], sb[i & 3]);
@@ -195,65 +206,75 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
                 T = __builtin_amdgcn_sad_hi_u8(B, w, T);
                 if (i >= 2 * R) {
                     const uint32_t old = (i == 2 * R) ? 0u : Tprev[(i - 2 * R - 1) % (2 * R + 1)];
-                    col[(i - 2 * R) * G::CSS] = T - old;
+                    col[(i - 2 * R - h * G::HALF) * G::CSS] = T - old;
                 }
                 Tprev[i % (2 * R + 1)] = T;
             }
-        }
-        // the CS plane is private to this wave: LDS ops of one wave complete in order, so only
-        // the compiler must not move the phase-H reads above the phase-V writes
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ================= phase H (lane = row x half-row) =================
-        {
-            const uint32_t* row = csw + hj * G::CSS + obase;
-            uint32_t v[4 * G::NCS4];
+            // the plane is private to this wave and one wave's LDS ops complete in order: only the
+            // compiler must keep phase-H reads below phase-V writes (and the next writes below them)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // ====== phase H (lane = half-row j x quarter q) ======
+            {
+                const uint32_t* row = csw + hj * G::CSS + obase;
+                uint32_t v[2 * G::NCS2];
 #pragma unroll
-            for (int q = 0; q < G::NCS4; ++q) {
-                const uint4 x4 = *reinterpret_cast<const uint4*>(row + 4 * q);
-                v[4 * q + 0] = x4.x; v[4 * q + 1] = x4.y; v[4 * q + 2] = x4.z; v[4 * q + 3] = x4.w;
-            }
-            const uint32_t dsel = (uint32_t)(d & 0xFF) | ((uint32_t)((d + 1) & 0xFF) << 8);
-            uint32_t S = 0u;
-#pragma unroll
-            for (int k = 0; k < 2 * R; ++k) S += v[k];
-            const bool dm = d_edge || (d + 1 >= d_hi);
-            if (!dm) {
-#pragma unroll
-                for (int o = 0; o < G::NOUT; ++o) {
-                    S += v[o + 2 * R];
-                    const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
-                    const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
-                    best[o] = min(best[o], min(klo, khi));
-                    S -= v[o];
+                for (int q = 0; q < G::NCS2; ++q) {
+                    const uint2 x2 = *reinterpret_cast<const uint2*>(row + 2 * q);
+                    v[2 * q + 0] = x2.x;
+                    v[2 * q + 1] = x2.y;
                 }
-            } else {
+                uint32_t S = 0u;
 #pragma unroll
-                for (int o = 0; o < G::NOUT; ++o) {
-                    S += v[o + 2 * R];
-                    const int x = x0 + obase + o;
-                    const int lim = a.valid_mode == 0 ? (W - x) : x;
-                    uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
-                    uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
-                    klo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
-                    khi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
-                    best[o] = min(best[o], min(klo, khi));
-                    S -= v[o];
+                for (int k = 0; k < 2 * R; ++k) S += v[k];
+                if (!dm) {
+#pragma unroll
+                    for (int o = 0; o < G::NQ; ++o) {
+                        S += v[o + 2 * R];
+                        const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                        const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                        best[h][o] = min(best[h][o], min(klo, khi));
+                        S -= v[o];
+                    }
+                } else {
+#pragma unroll
+                    for (int o = 0; o < G::NQ; ++o) {
+                        S += v[o + 2 * R];
+                        const int x = x0 + obase + o;
+                        const int lim = a.valid_mode == 0 ? (W - x) : x;
+                        uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                        uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                        klo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
+                        khi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
+                        best[h][o] = min(best[h][o], min(klo, khi));
+                        S -= v[o];
+                    }
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     __syncthreads();
 
-    // ---- fold the 4 pair-waves: best[w][j][o] through LDS, then min + store ----
-    {
-        uint32_t* bw = cs + wave * (kTileH * G::CSS) + hj * G::CSS + obase;
+    // ---- fold the 4 waves (same lane = same pixels in every wave) through one LDS plane ----
+    uint32_t* fold = cs;                                   // [kTileH][TW] keys
+    if (wave == 0) {
 #pragma unroll
-        for (int o = 0; o < G::NOUT; ++o) bw[o] = best[o];
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int o = 0; o < G::NQ; ++o)
+                if (obase + o < G::TW) fold[(h * G::HALF + hj) * G::TW + obase + o] = best[h][o];
+    }
+    __syncthreads();
+    if (wave != 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int o = 0; o < G::NQ; ++o)
+                if (obase + o < G::TW) atomicMin(&fold[(h * G::HALF + hj) * G::TW + obase + o], best[h][o]);
     }
     __syncthreads();
     uint8_t* Df = a.disp ? a.disp + (int64_t)frame * a.out_frame_stride : nullptr;
@@ -262,8 +283,7 @@ __global__ __launch_bounds__(kThreads, 3) void box_match_kernel(MatchArgs a, int
         const int j = e / G::TW, o = e - j * G::TW;
         const int y = y0 + j, x = x0 + o;
         if (y >= H || x >= W) continue;
-        const uint32_t* p = cs + j * G::CSS + o;
-        const uint32_t k = min(min(p[0], p[kTileH * G::CSS]), min(p[2 * kTileH * G::CSS], p[3 * kTileH * G::CSS]));
+        const uint32_t k = fold[e];
         if (Df) Df[(int64_t)y * a.out_pitch + x] = k < a.thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
         if (Kf) Kf[(int64_t)y * W + x] = k;
     }
