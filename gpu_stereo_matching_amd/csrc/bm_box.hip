@@ -117,6 +117,9 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
 
     // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8, from dword loads
     //      (all issued before any LDS write; image borders read as 0) ----
+#if SM_ABLATE & 8
+    if (false)
+#endif
     {
         constexpr int N = G::ROWS * G::NDW;
 #pragma unroll 4
@@ -259,6 +262,9 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
     }
     __syncthreads();
 
+#if SM_ABLATE & 4
+    if (a.W > 0) { if (tid == 0) a.disp[0] = (uint8_t)(best[0][0] ^ best[1][G::NQ - 1]); return; }
+#endif
     // ---- fold the 4 waves (same lane = same pixels in every wave) through one LDS plane ----
     uint32_t* fold = cs;                                   // [kTileH][TW] keys
     if (wave == 0) {

@@ -1,0 +1,18 @@
+"""Time the box kernel from an ablation build of libsm_hip.so (path as argv[1])."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+import gpu_stereo_matching_amd._capi as C
+C.load(sys.argv[1])
+import gpu_stereo_matching_amd as sm
+m = sm.BlockMatcher(0, 1920, 1080, 256)
+pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(4)]
+Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda(); Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+out = torch.empty_like(Lt)
+for _ in range(5): m.match_device(Lt, Rt, 5, 128, out_t=out)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(40): m.match_device(Lt, Rt, 5, 128, out_t=out)
+e1.record(); torch.cuda.synchronize()
+print(sys.argv[1], "ms/frame", e0.elapsed_time(e1) / 40 / 4)
