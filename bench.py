@@ -180,17 +180,19 @@ def main():
     if rank == 0 and not args.no_variants:
         variants = {}
         o1 = torch.empty_like(Lt[0])
-        for name, kw in (("box+lr", dict(lr_check=True)),):
+        for name, kw in (("box+lr", dict(lr_check=True)), ("guided", dict(agg="guided")),
+                         ("guided+lr", dict(agg="guided", lr_check=True))):
             try:
                 for _ in range(3):
                     m.match_device(Lt[0], Rt[0], r, D, out_t=o1, stream=stream, **kw)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                for _ in range(20):
+                nrep = 20 if "guided" not in name else 5
+                for _ in range(nrep):
                     m.match_device(Lt[0], Rt[0], r, D, out_t=o1, stream=stream, **kw)
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
-                ms = e0.elapsed_time(e1) / 20
+                ms = e0.elapsed_time(e1) / nrep
                 variants[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000 / ms, 2)}
             except Exception as e:  # report, never hide
                 variants[name] = {"error": str(e)}

@@ -7,7 +7,8 @@ namespace sm {
 
 // Per-handle scratch for the guided path (grown on demand, freed in sm_destroy).
 struct GuidedWorkspace {
-    float* stats = nullptr;   // [batch][2][H][W]: mean_I, 1/(var_I + eps)
+    static constexpr int kChunk = 16;   // disparities per a/b hand-off (a, b planes live in HBM/MALL)
+    float* stats = nullptr;             // [3][P] guide stats, [P] best q, [P] best d, [2*kChunk][P] a/b
     size_t stats_bytes = 0;
 };
 
