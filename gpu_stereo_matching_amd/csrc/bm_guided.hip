@@ -97,11 +97,24 @@ struct GeoAB {
     static constexpr int RBW = 64 + 64 + 8;                     // right band bytes per row (d chunk <= 64)
 };
 
+// a/b planes are stored tile-blocked so that each phase-H lane's run of outputs is contiguous
+// and 16-B aligned: plane[d][tile][row(32)][half(2)][32 floats]  (8 KB per tile per plane).
+constexpr int kABTile = kABRows * 64;
+
+template <int R>
+__device__ __forceinline__ int64_t ab_index(int y, int x, int tiles_x) {
+    using G = GeoAB<R>;
+    const int ty = y / kABRows, tx = x / G::TW;
+    const int xi = x - tx * G::TW;
+    const int half = xi / G::NOUT, xo = xi - half * G::NOUT;
+    return ((int64_t)(ty * tiles_x + tx) * kABTile) + (y - ty * kABRows) * 64 + half * 32 + xo;
+}
+
 template <int R>
 __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ Rimg,
                                                           int W, int H, int pitch, int d0, int nd,
                                                           const float* __restrict__ st, float* __restrict__ ab,
-                                                          int tiles_x) {
+                                                          int tiles_x, int tiles_y) {
     using G = GeoAB<R>;
     __shared__ uint8_t rband[G::ROWS][G::RBW];
     __shared__ uint32_t csp[4][kABRows][G::CSS];
@@ -129,7 +142,7 @@ __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restr
     // phase-H ownership: row hj, half hh -> outputs [hh*NOUT, hh*NOUT + NOUT)
     const int hj = lane & 31, hh = lane >> 5, obase = hh * G::NOUT;
     const int yo = y0 + hj;
-    // per-pixel d-independent constants in LDS: {N, SI, 1/(N^2 var + eps N^2), mean_I}
+    // per-pixel d-independent constants in LDS: {N, SI, 1/(N^2 var + eps N^2), 1/N}
     for (int e = tid; e < kABRows * G::TW; e += kT) {
         const int i = e / G::TW, j = e % G::TW;
         const int y = y0 + i, x = x0 + j;
@@ -139,7 +152,7 @@ __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restr
             const uint32_t si = (uint32_t)__float_as_int(st[p]);
             const float in = st[2 * P + p];
             v = make_uint4((uint32_t)(win_count(x, R, W) * win_count(y, R, H)), si, __float_as_uint(st[P + p]),
-                           __float_as_uint((float)si * in));
+                           __float_as_uint(in));
         }
         pix[i][j] = v;
     }
@@ -176,8 +189,10 @@ __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restr
                 sp += v & 0xFFFu;
                 sip += v >> 12;
             }
-            float* ap = ab + (int64_t)(2 * dd) * P;
-            float* bp = ab + (int64_t)(2 * dd + 1) * P;
+            const int64_t plane = (int64_t)tiles_x * tiles_y * kABTile;
+            float* ap = ab + (int64_t)(2 * dd) * plane + (int64_t)blockIdx.x * kABTile + hj * 64 + hh * 32;
+            float* bp = ab + (int64_t)(2 * dd + 1) * plane + (int64_t)blockIdx.x * kABTile + hj * 64 + hh * 32;
+            float av[(G::NOUT + 3) & ~3], bv[(G::NOUT + 3) & ~3];
 #pragma unroll
             for (int o = 0; o < G::NOUT; ++o) {
                 const uint32_t vin = row[o + 2 * R];
@@ -187,16 +202,18 @@ __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restr
                 const uint4 pc = pix[hj][obase + o < G::TW ? obase + o : 0];
                 const int32_t num = (int32_t)(pc.x * sip - pc.y * sp);
                 const float a = (float)num * __uint_as_float(pc.z);
-                const float b = (float)sp / (float)pc.x - a * __uint_as_float(pc.w);
-                const int x = x0 + obase + o;
-                if (yo < H && x < W && obase + o < G::TW) {
-                    const int64_t p = (int64_t)yo * W + x;
-                    ap[p] = a;
-                    bp[p] = b;
-                }
+                av[o] = a;
+                bv[o] = ((float)sp - a * (float)pc.y) * __uint_as_float(pc.w);   // (Sp - a SI) / N
                 const uint32_t vout = row[o];
                 sp -= vout & 0xFFFu;
                 sip -= vout >> 12;
+            }
+#pragma unroll
+            for (int o = G::NOUT; o < ((G::NOUT + 3) & ~3); ++o) av[o] = bv[o] = 0.f;
+#pragma unroll
+            for (int q = 0; q < ((G::NOUT + 3) & ~3) / 4; ++q) {
+                *reinterpret_cast<float4*>(ap + 4 * q) = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+                *reinterpret_cast<float4*>(bp + 4 * q) = make_float4(bv[4 * q], bv[4 * q + 1], bv[4 * q + 2], bv[4 * q + 3]);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -213,7 +230,8 @@ template <int R>
 __global__ __launch_bounds__(kT) void guided_wta_kernel(const uint8_t* __restrict__ L, int W, int H, int pitch,
                                                         int d0, int nd, const float* __restrict__ ab,
                                                         const float* __restrict__ st, int valid_mode,
-                                                        float* __restrict__ best, int* __restrict__ bd) {
+                                                        float* __restrict__ best, int* __restrict__ bd,
+                                                        int ab_tiles_x, int ab_tiles_y) {
     __shared__ float ta[kGTH + 2 * R][kGTW + 2 * R + 1];
     __shared__ float tb[kGTH + 2 * R][kGTW + 2 * R + 1];
     __shared__ float va[kGTH][kGTW + 2 * R + 1];
@@ -238,14 +256,15 @@ __global__ __launch_bounds__(kT) void guided_wta_kernel(const uint8_t* __restric
     }
     for (int dd = 0; dd < nd; ++dd) {
         const int d = d0 + dd;
-        const float* ap = ab + (int64_t)(2 * dd) * P;
-        const float* bp = ab + (int64_t)(2 * dd + 1) * P;
+        const int64_t plane = (int64_t)ab_tiles_x * ab_tiles_y * kABTile;
+        const float* ap = ab + (int64_t)(2 * dd) * plane;
+        const float* bp = ab + (int64_t)(2 * dd + 1) * plane;
         __syncthreads();
         for (int e = threadIdx.x; e < (kGTH + 2 * R) * (kGTW + 2 * R); e += kT) {
             const int i = e / (kGTW + 2 * R), j = e % (kGTW + 2 * R);
             const int y = y0 - R + i, x = x0 - R + j;
             const bool ok = y >= 0 && y < H && x >= 0 && x < W;
-            const int64_t p = ok ? (int64_t)y * W + x : 0;
+            const int64_t p = ok ? ab_index<R>(y, x, ab_tiles_x) : 0;
             ta[i][j] = ok ? ap[p] : 0.f;
             tb[i][j] = ok ? bp[p] : 0.f;
         }
@@ -324,9 +343,9 @@ hipError_t run_r(GuidedWorkspace& ws, const uint8_t* L, const uint8_t* Rimg, int
     for (int d0 = 0; d0 < D; d0 += GuidedWorkspace::kChunk) {
         const int nd = D - d0 < GuidedWorkspace::kChunk ? D - d0 : GuidedWorkspace::kChunk;
         hipLaunchKernelGGL((guided_ab_kernel<R>), dim3(tiles_x * tiles_y), dim3(kT), 0, s, L, Rimg, W, H, pitch, d0,
-                           nd, st, ab, tiles_x);
+                           nd, st, ab, tiles_x, tiles_y);
         hipLaunchKernelGGL((guided_wta_kernel<R>), dim3((W + kGTW - 1) / kGTW, (H + kGTH - 1) / kGTH), dim3(kT), 0,
-                           s, L, W, H, pitch, d0, nd, ab, st, valid_mode, best, bd);
+                           s, L, W, H, pitch, d0, nd, ab, st, valid_mode, best, bd, tiles_x, tiles_y);
     }
     hipLaunchKernelGGL(guided_final_kernel, dim3((W + 255) / 256, H), dim3(256), 0, s, bd, W, H, disp, out_pitch);
     return hipGetLastError();
@@ -345,7 +364,9 @@ hipError_t launch_guided_match(GuidedWorkspace& ws, const uint8_t* L, const uint
                                uint8_t* disp, int out_pitch, int64_t out_frame_stride, hipStream_t s) {
     if (radius < 0 || radius > kMaxFastRadius) return hipErrorInvalidValue;
     const int64_t P = (int64_t)W * H;
-    const size_t need = (size_t)P * (5 + 2 * GuidedWorkspace::kChunk) * sizeof(float);
+    const int64_t tiles = (int64_t)((W + 64 - 2 * radius - 1) / (64 - 2 * radius)) * ((H + kABRows - 1) / kABRows);
+    const int64_t plane = tiles * kABTile;
+    const size_t need = (size_t)(5 * P + 2 * GuidedWorkspace::kChunk * plane) * sizeof(float);
     if (ws.stats_bytes < need) {
         guided_workspace_free(ws);
         hipError_t e = hipMalloc(&ws.stats, need);
