@@ -313,6 +313,244 @@ __global__ __launch_bounds__(kT) void guided_wta_kernel(const uint8_t* __restric
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// guided_fused: the whole guided pipeline for one output tile, every d, inside LDS.
+//   P region (cost sums)   : 64 columns (one per lane) x (TH + 4R) rows, image cols x0-2R ..
+//   A region (a, b)        : (TW + 2R) x (TH + 2R), image (x0-R, y0-R) ..
+//   output tile            : TW = 64 - 4R  x  TH = 32
+// Per d (4 block barriers):
+//   S1V  lane = P column; waves split the A rows: packed prefix T += AD*(1 + 4096 L) -> CS rows
+//   S1H  thread = (A row, segment): running Sp / SIp -> a, b  (exact integer numerators)
+//   S2V  thread = (A column, 8-row group): running float sums of a, b over 2R+1 rows
+//   S2H  thread = (output row, segment): running sums -> q = f(a) I + f(b) -> WTA in registers
+// The guide statistics (SI = sum L, SII = sum L^2) come from the same S1V/S1H with R := 0
+// (AD = L, L*AD = L^2), once per tile.
+// ----------------------------------------------------------------------------------------
+template <int R>
+struct GeoF {
+    static constexpr int TW = 64 - 4 * R;
+    static constexpr int TH = 32;
+    static constexpr int AW = TW + 2 * R;
+    static constexpr int AH = TH + 2 * R;
+    static constexpr int PH = TH + 4 * R;
+    static constexpr int RPW = (AH + 3) / 4;                 // A rows per wave in S1V
+    static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
+    static constexpr int NSEG1 = 256 / AH;                   // S1H segments per A row
+    static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
+    static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
+    static constexpr int CSS = ((NSEG1 * SW1 + 2 * R) > 64 ? (NSEG1 * SW1 + 2 * R) : 64) + 4;
+    static constexpr int MS = ((8 * SW2 + 2 * R) > AW ? (8 * SW2 + 2 * R) : AW) + 1;
+    static constexpr int ABS = AW + 1;
+    static constexpr int RBW = 64 + 256 + 8;                 // right band bytes per P row (D <= 256)
+    static constexpr int CSM = (AH * CSS * 4 > TH * MS * 8 ? AH * CSS * 4 : TH * MS * 8);
+    static constexpr int LT = PH * 64;                       // staged left tile bytes (aliases CSM)
+    static constexpr int CSM_BYTES = ((CSM > LT ? CSM : LT) + 15) & ~15;
+    static constexpr int AB_BYTES = AH * ABS * 8;
+    static constexpr int RB_BYTES = (PH * RBW + 15) & ~15;
+    static constexpr int LDS = CSM_BYTES + AB_BYTES + RB_BYTES;
+};
+
+template <int R>
+__global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ Rimg,
+                                                             int W, int H, int pitch, int D, float eps, int valid_mode,
+                                                             uint8_t* __restrict__ disp, int out_pitch, int tiles_x) {
+    using G = GeoF<R>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                           // [AH][CSS] packed sums
+    float2* mm = reinterpret_cast<float2*>(smem);                               // [TH][MS]  (aliases cs)
+    uint8_t* lt = smem;                                                          // [PH][64]  (aliases cs)
+    float2* abp = reinterpret_cast<float2*>(smem + G::CSM_BYTES);               // [AH][ABS]
+    uint8_t* rb = smem + G::CSM_BYTES + G::AB_BYTES;                             // [PH][RBW]
+
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int x0 = tx * G::TW, y0 = ty * G::TH;
+    const int px0 = x0 - 2 * R, py0 = y0 - 2 * R;      // P region origin (image coords)
+    const int rbase = px0 - 256;                      // image column of rb[.][0]
+
+    // ---- stage right band (all d) and left P tile ----
+    for (int e = tid; e < G::PH * (G::RBW / 4); e += kT) {
+        const int i = e / (G::RBW / 4), j = e % (G::RBW / 4);
+        const int y = py0 + i;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int x = rbase + 4 * j + b;
+            if (y >= 0 && y < H && x >= 0 && x < W) v |= (uint32_t)Rimg[(int64_t)y * pitch + x] << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = v;
+    }
+    for (int e = tid; e < G::PH * 16; e += kT) {
+        const int i = e / 16, j = e % 16;
+        const int y = py0 + i;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int x = px0 + 4 * j + b;
+            if (y >= 0 && y < H && x >= 0 && x < W) v |= (uint32_t)L[(int64_t)y * pitch + x] << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = v;
+    }
+    __syncthreads();
+    // S1V state: this wave walks P rows [a0, a0 + NV); lane = P column c
+    const int a0 = wave * G::RPW;
+    const int c = lane;
+    const int xc = px0 + c;
+    const bool col_in = xc >= 0 && xc < W;
+    uint32_t lz[G::NV];
+#pragma unroll
+    for (int t = 0; t < G::NV; ++t) lz[t] = (a0 + t < G::PH) ? (uint32_t)lt[(a0 + t) * 64 + c] : 0u;
+    __syncthreads();   // lt (aliased with cs) is consumed
+
+    // S1H ownership: A row h1i, segment h1s (threads >= AH*NSEG1 idle in S1H)
+    const bool h1_on = tid < G::AH * G::NSEG1;
+    const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
+    const int h1y = y0 - R + h1i;
+    // S2V ownership: A column v2j, output rows [8*v2g, 8*v2g + 8)
+    const bool v2_on = tid < 4 * G::AW;
+    const int v2g = v2_on ? tid / G::AW : 0, v2j = v2_on ? tid % G::AW : 0;
+    // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2)
+    const int h2r = tid >> 3, h2s = tid & 7;
+    const int oy = y0 + h2r;
+
+    // per-A-pixel constants (filled by the stats pass) and per-output WTA state
+    uint32_t nN[G::SW1], nSI[G::SW1];
+    float invden[G::SW1], invN[G::SW1];
+    float oI[G::SW2], oinvN[G::SW2], bq[G::SW2];
+    int bdd[G::SW2];
+#pragma unroll
+    for (int o = 0; o < G::SW2; ++o) {
+        const int x = x0 + h2s * G::SW2 + o;
+        const bool ok = oy < H && x < W && h2s * G::SW2 + o < G::TW;
+        oI[o] = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
+        oinvN[o] = ok ? 1.0f / (float)(win_count(x, R, W) * win_count(oy, R, H)) : 0.f;
+        bq[o] = valid_mode == 0 ? 50.0f : __builtin_huge_valf();
+        bdd[o] = -256;
+    }
+
+    for (int d = -1; d < D; ++d) {              // d = -1: guide statistics pass
+        // ================= S1V =================
+        {
+            const bool m = d < 0 ? true : (col_in && xc >= d);
+            const uint8_t* rc = rb + (c - (d < 0 ? 0 : d) + 256);
+            uint32_t T = 0u, Tp[2 * R + 1];
+#pragma unroll
+            for (int t = 0; t < G::NV; ++t) {
+                const int i = a0 + t;                                   // P row
+                const uint32_t rv = (d < 0 || i >= G::PH) ? 0u : (uint32_t)rc[i * G::RBW];
+                uint32_t ad = __builtin_amdgcn_sad_u8(lz[t], rv, 0u);
+                ad = m ? ad : 0u;
+                T += __umul24(ad, (lz[t] << 12) | 1u);
+                if (t >= 2 * R) {
+                    const uint32_t old = (t == 2 * R) ? 0u : Tp[(t - 2 * R - 1) % (2 * R + 1)];
+                    const int j = i - 2 * R;                            // A row
+                    if (j < a0 + G::RPW && j < G::AH) cs[j * G::CSS + c] = T - old;
+                }
+                Tp[t % (2 * R + 1)] = T;
+            }
+        }
+        __syncthreads();
+        // ================= S1H =================
+        if (h1_on) {
+            const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
+            uint32_t sp = 0, sip = 0;
+#pragma unroll
+            for (int k = 0; k < 2 * R; ++k) {
+                const uint32_t v = row[k];
+                sp += v & 0xFFFu;
+                sip += v >> 12;
+            }
+#pragma unroll
+            for (int o = 0; o < G::SW1; ++o) {
+                const uint32_t vin = row[o + 2 * R];
+                sp += vin & 0xFFFu;
+                sip += vin >> 12;
+                const int j = h1s * G::SW1 + o;                         // A column
+                const int x = x0 - R + j;
+                const bool inimg = h1y >= 0 && h1y < H && x >= 0 && x < W && j < G::AW;
+                if (d < 0) {
+                    // guide statistics: sp = SI, sip = SII
+                    const uint32_t N = inimg ? (uint32_t)(win_count(x, R, W) * win_count(h1y, R, H)) : 1u;
+                    const int32_t nvar = (int32_t)(N * sip - sp * sp);
+                    nN[o] = N;
+                    nSI[o] = sp;
+                    invden[o] = 1.0f / ((float)nvar + eps * (float)N * (float)N);
+                    invN[o] = inimg ? 1.0f / (float)N : 0.f;
+                } else if (j < G::AW) {
+                    const int32_t num = (int32_t)(nN[o] * sip - nSI[o] * sp);
+                    const float a = (float)num * invden[o];
+                    const float b = ((float)sp - a * (float)nSI[o]) * invN[o];
+                    abp[h1i * G::ABS + j] = inimg ? make_float2(a, b) : make_float2(0.f, 0.f);
+                }
+                const uint32_t vout = row[o];
+                sp -= vout & 0xFFFu;
+                sip -= vout >> 12;
+            }
+        }
+        if (d < 0) {
+            __syncthreads();
+            continue;
+        }
+        __syncthreads();
+        // ================= S2V =================
+        if (v2_on) {
+            const float2* col = abp + v2j;
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int k = 0; k < 2 * R; ++k) {
+                const float2 v = col[(8 * v2g + k) * G::ABS];
+                sa += v.x;
+                sb += v.y;
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float2 vin = col[(8 * v2g + r + 2 * R) * G::ABS];
+                sa += vin.x;
+                sb += vin.y;
+                mm[(8 * v2g + r) * G::MS + v2j] = make_float2(sa, sb);
+                const float2 vout = col[(8 * v2g + r) * G::ABS];
+                sa -= vout.x;
+                sb -= vout.y;
+            }
+        }
+        __syncthreads();
+        // ================= S2H + WTA =================
+        {
+            const float2* row = mm + h2r * G::MS + h2s * G::SW2;
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int k = 0; k < 2 * R; ++k) {
+                const float2 v = row[k];
+                sa += v.x;
+                sb += v.y;
+            }
+#pragma unroll
+            for (int o = 0; o < G::SW2; ++o) {
+                const float2 vin = row[o + 2 * R];
+                sa += vin.x;
+                sb += vin.y;
+                const float q = (sa * oI[o] + sb) * oinvN[o];
+                const int x = x0 + h2s * G::SW2 + o;
+                const int lim = valid_mode == 0 ? (W - x) : x;
+                if (d <= lim && q < bq[o]) {
+                    bq[o] = q;
+                    bdd[o] = d;
+                }
+                const float2 vout = row[o];
+                sa -= vout.x;
+                sb -= vout.y;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int o = 0; o < G::SW2; ++o) {
+        const int x = x0 + h2s * G::SW2 + o;
+        if (oy < H && x < W && h2s * G::SW2 + o < G::TW)
+            disp[(int64_t)oy * out_pitch + x] = (uint8_t)(bdd[o] & 0xFF);   // (uchar)dm, Device.cu:63
+    }
+}
+
 __global__ __launch_bounds__(256) void guided_init_kernel(float* best, int* bd, int64_t P, float seed) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < P) {
@@ -351,6 +589,16 @@ hipError_t run_r(GuidedWorkspace& ws, const uint8_t* L, const uint8_t* Rimg, int
     return hipGetLastError();
 }
 
+template <int R>
+hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int D, float eps, int valid_mode,
+                     uint8_t* disp, int out_pitch, hipStream_t s) {
+    using G = GeoF<R>;
+    const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
+    hipLaunchKernelGGL((guided_fused_kernel<R>), dim3(tiles_x * tiles_y), dim3(kT), (size_t)G::LDS, s, L, Rimg, W, H,
+                       pitch, D, eps, valid_mode, disp, out_pitch, tiles_x);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 void guided_workspace_free(GuidedWorkspace& ws) {
@@ -363,6 +611,7 @@ hipError_t launch_guided_match(GuidedWorkspace& ws, const uint8_t* L, const uint
                                int batch, int64_t frame_stride, int radius, int D, float eps, int valid_mode,
                                uint8_t* disp, int out_pitch, int64_t out_frame_stride, hipStream_t s) {
     if (radius < 0 || radius > kMaxFastRadius) return hipErrorInvalidValue;
+    if (D > 256) return hipErrorInvalidValue;
     const int64_t P = (int64_t)W * H;
     const int64_t tiles = (int64_t)((W + 64 - 2 * radius - 1) / (64 - 2 * radius)) * ((H + kABRows - 1) / kABRows);
     const int64_t plane = tiles * kABTile;
@@ -373,11 +622,26 @@ hipError_t launch_guided_match(GuidedWorkspace& ws, const uint8_t* L, const uint
         if (e != hipSuccess) return e;
         ws.stats_bytes = need;
     }
+    static const bool use_fused = [] { const char* e = std::getenv("SM_GUIDED_UNFUSED"); return !(e && e[0] == '1'); }();
     for (int f = 0; f < batch; ++f) {
         const uint8_t* Lf = L + (int64_t)f * frame_stride;
         const uint8_t* Rf = R + (int64_t)f * frame_stride;
         uint8_t* Df = disp + (int64_t)f * out_frame_stride;
         hipError_t e;
+        if (use_fused) {
+            switch (radius) {
+                case 0: e = run_fused<0>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 1: e = run_fused<1>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 2: e = run_fused<2>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 3: e = run_fused<3>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 4: e = run_fused<4>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 5: e = run_fused<5>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                case 6: e = run_fused<6>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+                default: e = run_fused<7>(Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
+            }
+            if (e != hipSuccess) return e;
+            continue;
+        }
         switch (radius) {
             case 0: e = run_r<0>(ws, Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
             case 1: e = run_r<1>(ws, Lf, Rf, W, H, pitch, D, eps, valid_mode, Df, out_pitch, s); break;
