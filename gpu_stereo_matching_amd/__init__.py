@@ -110,6 +110,40 @@ class BlockMatcher:
                                                    mask.ctypes.data, W))
         return out, rd, mask
 
+    def match_bgr(self, left_bgr, right_bgr, radius: int, num_disp: int, agg: str = "box",
+                  lr_check: bool = False) -> np.ndarray:
+        """imread -> cvtColor(BGR2GRAY) -> blockMatching_gpu in one call (Caller.cpp:12-19): HxWx3/4
+        uint8 BGR(A) frames in, uint8 disparity out; the gray conversion runs on the GPU."""
+        Lb = np.ascontiguousarray(left_bgr, dtype=np.uint8)
+        Rb = np.ascontiguousarray(right_bgr, dtype=np.uint8)
+        if Lb.ndim != 3 or Lb.shape[2] not in (3, 4) or Lb.shape != Rb.shape:
+            raise ValueError("expected two equal HxWx3 or HxWx4 uint8 BGR(A) frames")
+        H, W, C = Lb.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_block_match_bgr_u8(self._h, Lb.ctypes.data, Rb.ctypes.data, W, H, W * C, C, radius,
+                                                    num_disp, _flags(agg, lr_check), out.ctypes.data, W))
+        return out
+
+    def bgr_to_gray_device(self, bgr_t, out_t=None, stream=None):
+        """[H, W, 3|4] uint8 cuda tensor -> [H, W] gray (OpenCV 2.4 fixed point), async on `stream`."""
+        import torch
+        H, W, C = bgr_t.shape
+        if out_t is None:
+            out_t = torch.empty((H, W), dtype=torch.uint8, device=bgr_t.device)
+        _capi.check(self._lib.sm_bgr_to_gray_device(self._h, bgr_t.data_ptr(), W, H, W * C, C, out_t.data_ptr(), W,
+                                                    self._stream_ptr(stream)))
+        return out_t
+
+    def remap_device(self, src_t, mapx_t, mapy_t, out_t=None, stream=None):
+        """Rectification remap (Device.cu:127-167): src [H, W] uint8, maps [H, W] float32 (CV_32FC1)."""
+        import torch
+        H, W = src_t.shape
+        if out_t is None:
+            out_t = torch.empty_like(src_t)
+        _capi.check(self._lib.sm_remap_u8_device(self._h, src_t.data_ptr(), W, H, W, mapx_t.data_ptr(),
+                                                 mapy_t.data_ptr(), W, out_t.data_ptr(), W, self._stream_ptr(stream)))
+        return out_t
+
     def stage_ms(self) -> Tuple[float, float, float]:
         """(upload, match, download) ms of the last host call (Device.cu:218,238/257,292)."""
         u, m, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()

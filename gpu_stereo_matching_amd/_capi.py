@@ -29,6 +29,7 @@ EXPORTED = (
     "sm_version", "sm_last_error_string", "sm_device_count", "sm_create", "sm_destroy",
     "sm_set_param_f", "sm_block_match_u8", "sm_block_match_lr_u8", "sm_last_stage_ms",
     "sm_match_device", "sm_slice_keys_device", "sm_keys_to_disp_device", "sm_stream_sync",
+    "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8",
 )
 
 
@@ -74,6 +75,9 @@ def load(path: str = LIB_PATH):
     L.sm_slice_keys_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp, vp]
     L.sm_keys_to_disp_device.argtypes = [vp, vp, i, i, i, vp, i, vp]
     L.sm_stream_sync.argtypes = [vp, vp]
+    L.sm_bgr_to_gray_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
+    L.sm_remap_u8_device.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i, vp]
+    L.sm_block_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

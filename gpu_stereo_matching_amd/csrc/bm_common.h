@@ -38,4 +38,9 @@ hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride
                            uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
                            hipStream_t s);
 
+hipError_t launch_bgr_to_gray(const uint8_t* src, int W, int H, int pitch, int channels, uint8_t* dst, int dpitch,
+                              hipStream_t s);
+hipError_t launch_remap(const uint8_t* src, int W, int H, int pitch, const float* mapx, const float* mapy, int mpitch,
+                        uint8_t* dst, int dpitch, hipStream_t s);
+
 }  // namespace sm

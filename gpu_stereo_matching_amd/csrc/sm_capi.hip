@@ -28,6 +28,9 @@ struct sm_handle {
     // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
     uint8_t* d_lr = nullptr;
     size_t lr_bytes = 0;
+    // BGR staging for sm_block_match_bgr_u8 (grown on demand)
+    uint8_t* d_bgr = nullptr;
+    size_t bgr_bytes = 0;
     // guided workspace
     sm::GuidedWorkspace gws;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
@@ -256,6 +259,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_right);
     (void)hipFree(h->d_disp);
     (void)hipFree(h->d_lr);
+    (void)hipFree(h->d_bgr);
     sm::guided_workspace_free(h->gws);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -350,10 +354,76 @@ SM_API int sm_keys_to_disp_device(sm_handle* h, const uint32_t* d_keys, int widt
     return SM_OK;
 }
 
+SM_API int sm_bgr_to_gray_device(sm_handle* h, const uint8_t* d_bgr, int width, int height, int pitch, int channels,
+                                 uint8_t* d_gray, int gray_pitch, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_bgr || !d_gray || width <= 0 || height <= 0 || (channels != 3 && channels != 4) ||
+        pitch < width * channels || gray_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad bgr_to_gray arguments");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_bgr_to_gray(d_bgr, width, height, pitch, channels, d_gray, gray_pitch, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_remap_u8_device(sm_handle* h, const uint8_t* d_src, int width, int height, int pitch,
+                              const float* d_mapx, const float* d_mapy, int map_pitch, uint8_t* d_dst, int dst_pitch,
+                              void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_src || !d_mapx || !d_mapy || !d_dst || width <= 0 || height <= 0 || pitch < width || map_pitch < width ||
+        dst_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad remap arguments");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_remap(d_src, width, height, pitch, d_mapx, d_mapy, map_pitch, d_dst, dst_pitch,
+                            (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
+                                 int height, int pitch, int channels, int radius, int num_disp, unsigned flags,
+                                 uint8_t* disp_out, int out_pitch) {
+    int rc = check_geometry(h, width, height, width, radius, num_disp);
+    if (rc) return rc;
+    if (!left_bgr || !right_bgr || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if ((channels != 3 && channels != 4) || pitch < width * channels || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad BGR layout");
+    if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame exceeds handle capacity");
+    SM_HIP(hipSetDevice(h->device));
+    const size_t row = (size_t)width * channels, need = 2 * row * height;
+    if (h->bgr_bytes < need) {
+        if (h->d_bgr) (void)hipFree(h->d_bgr);
+        h->d_bgr = nullptr;
+        h->bgr_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_bgr, need));
+        h->bgr_bytes = need;
+    }
+    hipStream_t s = h->stream;
+    uint8_t* dl = h->d_bgr;
+    uint8_t* dr = h->d_bgr + row * height;
+    const int64_t P = (int64_t)width * height;
+    SM_HIP(hipEventRecord(h->ev[0], s));
+    SM_HIP(hipMemcpy2DAsync(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipMemcpy2DAsync(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipEventRecord(h->ev[1], s));
+    SM_HIP(sm::launch_bgr_to_gray(dl, width, height, (int)row, channels, h->d_left, width, s));
+    SM_HIP(sm::launch_bgr_to_gray(dr, width, height, (int)row, channels, h->d_right, width, s));
+    rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
+                    nullptr, nullptr, width, P, s);
+    if (rc) return rc;
+    SM_HIP(hipEventRecord(h->ev[2], s));
+    SM_HIP(hipMemcpy2DAsync(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipEventRecord(h->ev[3], s));
+    SM_HIP(hipEventSynchronize(h->ev[3]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
+    SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    return SM_OK;
+}
+
 SM_API int sm_stream_sync(sm_handle* h, void* stream) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
     SM_HIP(hipSetDevice(h->device));
-    SM_HIP(hipStreamSynchronize((hipStream_t)stream));
+    SM_HIP(hipStreamSynchronize(stream ? (hipStream_t)stream : h->stream));
     return SM_OK;
 }
 

@@ -108,8 +108,27 @@ SM_API int sm_slice_keys_device(sm_handle *h, const uint8_t *d_left, const uint8
 SM_API int sm_keys_to_disp_device(sm_handle *h, const uint32_t *d_keys, int width, int height,
                                   int radius, uint8_t *d_disp, int out_pitch, void *stream);
 
-/* Async host<->device helpers on the handle's stream (pinned staging is internal). */
+/* Wait for all work queued on `stream` (NULL = the handle's own stream). */
 SM_API int sm_stream_sync(sm_handle *h, void *stream);
+
+/* ---- caller-side steps in front of the path (SURVEY §8f "next") ----
+ * BGR(A) -> gray exactly as the reference's caller does it (Caller.cpp:15-16, OpenCV 2.4
+ * cvtColor CV_BGR2GRAY, 8-bit fixed point): Y = (1868 B + 9617 G + 4899 R + 8192) >> 14.
+ * `channels` is 3 (BGR) or 4 (BGRA; alpha ignored). */
+SM_API int sm_bgr_to_gray_device(sm_handle *h, const uint8_t *d_bgr, int width, int height, int pitch,
+                                 int channels, uint8_t *d_gray, int gray_pitch, void *stream);
+
+/* Rectification remap with CV_32FC1 maps, the reference's kernalRemap (Device.cu:127-167):
+ * bilinear, out-of-range taps -> 0, round half to even + saturate.  map_pitch in floats. */
+SM_API int sm_remap_u8_device(sm_handle *h, const uint8_t *d_src, int width, int height, int pitch,
+                              const float *d_mapx, const float *d_mapy, int map_pitch,
+                              uint8_t *d_dst, int dst_pitch, void *stream);
+
+/* imread -> cvtColor -> blockMatching_gpu in one call (Caller.cpp:12-19): BGR(A) host frames
+ * are uploaded, converted to gray on the GPU and matched.  Synchronous. */
+SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,
+                                 int width, int height, int pitch, int channels, int radius,
+                                 int num_disp, unsigned flags, uint8_t *disp_out, int out_pitch);
 
 #ifdef __cplusplus
 }

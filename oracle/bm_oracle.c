@@ -38,6 +38,37 @@ ORA_API void ora_bgr_to_gray(const uint8_t *bgr, int64_t npix, int channels, uin
 }
 
 /* ------------------------------------------------------------------------- */
+/* next: rectification remap, the reference's CPU twin   */
+/* CPU_Remap + CPU_BilinearInterpolation (Utility.cpp:239-264), identical    */
+/* to kernalRemap/BilinearInterpolation (Device.cu:127-167):                 */
+/*   x = map_y (row), y = map_x (col); taps outside [0,rows-1]x[0,cols-1]     */
+/*   -> 0; value = bilinear blend evaluated in float exactly as written       */
+/*   (no FMA contraction: built with -ffp-contract=off); saturate_cast<uchar> */
+/*   = round half to even + clamp.                                            */
+/* ------------------------------------------------------------------------- */
+static float ora_bilinear(const uint8_t *src, int rows, int cols, float x, float y)
+{
+    int x1 = (int)floorf(x), y1 = (int)floorf(y), x2 = x1 + 1, y2 = y1 + 1;
+    if (x1 < 0 || x2 >= rows || y1 < 0 || y2 >= cols) return 0.0f;
+    float q11 = src[x1 * cols + y1], q12 = src[x1 * cols + y2], q21 = src[x2 * cols + y1], q22 = src[x2 * cols + y2];
+    float left = (x2 - x) * q11 + (x - x1) * q21;
+    float right = (x2 - x) * q12 + (x - x1) * q22;
+    return (y2 - y) * left + (y - y1) * right;
+}
+
+ORA_API void ora_remap(const uint8_t *src, int W, int H, const float *mapx, const float *mapy, uint8_t *dst)
+{
+    for (int row = 0; row < H; ++row)
+        for (int col = 0; col < W; ++col) {
+            float v = ora_bilinear(src, H, W, mapy[row * W + col], mapx[row * W + col]);
+            float r = rintf(v);
+            if (!(r > 0.0f)) r = 0.0f;
+            if (r > 255.0f) r = 255.0f;
+            dst[row * W + col] = (uint8_t)r;
+        }
+}
+
+/* ------------------------------------------------------------------------- */
 /* a1: absolute-difference volume.                                           */
 /* PreCal BlockMatching.cpp:89-109 / kernalPreCal_V2 Device.cu:19-32:        */
 /*   dif[d][p] = |L[p] - R[p-d]| when (p mod W) >= d, else left at the       */

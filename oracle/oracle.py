@@ -55,6 +55,8 @@ def lib():
                                       ctypes.c_double, _u8p, _f64p, _f64p]
         L.ora_guided_disp.restype = ctypes.c_int
         L.ora_box_mean_f64.argtypes = [_f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p]
+        L.ora_remap.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                ctypes.POINTER(ctypes.c_float), _u8p]
         L.ora_synth_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
         _lib = L
     return _lib
@@ -170,6 +172,18 @@ def guided_disp(left, right, radius: int, D: int, eps: float, want_q: bool = Fal
     if rc != 0:
         raise MemoryError("ora_guided_disp")
     return (out, q, best) if want_q else (out, best)
+
+
+def remap(src, mapx, mapy):
+    """CPU_Remap restatement (Utility.cpp:239-264)."""
+    src = _img(src)
+    H, W = src.shape
+    mapx = np.ascontiguousarray(mapx, dtype=np.float32)
+    mapy = np.ascontiguousarray(mapy, dtype=np.float32)
+    out = np.empty((H, W), np.uint8)
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib().ora_remap(_p(src, _u8p), W, H, mapx.ctypes.data_as(fp), mapy.ctypes.data_as(fp), _p(out, _u8p))
+    return out
 
 
 def synth_pair(seed: int, W: int, H: int, D: int):
