@@ -9,7 +9,7 @@ timeout -k 10 900 python tools/pmc_traffic.py box_r5_1080p > gpurun_out/${TAG}_p
  && timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
  && cat gpurun_out/${TAG}_bench.json \
  && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/${TAG}_prof_bench.json 2>&1 \
- && cp gpurun_out/${TAG}_bench.json profiles/${TAG}_bench.json \
+ \
  && cp $(find gpurun_out/${TAG}_prof -name '*kernel_stats.csv' | head -1) profiles/${TAG}_bench_kernel_stats.csv \
  && cp gpurun_out/${TAG}_prof_bench.json profiles/${TAG}_bench_under_rocprof.json \
  && echo PROFILE_OK
