@@ -15,7 +15,9 @@
 //
 // Tile geometry (R = radius, compile-time for R <= 7):
 //   64 CS columns (one per lane) -> TW = 64 - 2R output columns, TH = 32 output rows.
-//   A chunk of 8 disparities = 4 pairs; wave w owns pair w in both phases.
+//   Disparities are processed in pairs; wave w of NW owns the contiguous pair range
+//   [w*npairs/NW, (w+1)*npairs/NW) end to end (phase V -> its private CS plane -> phase H), so
+//   the main loop has no workgroup barrier; the NW partial argmins are folded once at the end.
 //   Phase V (lane = column): T += |L - R_d| in the low u16 and |L - R_{d+1}| in the high u16
 //     (v_sad_u8 / v_sad_hi_u8); CS = T_i - T_{i-2R-1} (column window sums, two d per dword).
 //   Phase H (lane = row x half-row): running window sum along x over the packed pairs, keys
@@ -25,13 +27,26 @@
 namespace sm {
 namespace {
 
-constexpr int kThreads = 256;
+// waves per workgroup: 4 for the plain matcher (34 KB LDS, 4 WGs/CU); 8 for the fused right view,
+// whose extra 25 KB right-key rows are then shared by 8 waves (2 WGs/CU = the same 16 waves/CU)
+// (r = 0 and r = 7 keep 4 waves: their fused loops need > 128 VGPRs, so they run at 2 waves/SIMD
+// without spills)
+template <bool RIGHT, int R>
+constexpr bool kWideRight = RIGHT && R >= 1 && R <= 6;
+template <bool RIGHT, int R>
+constexpr int kWaves = kWideRight<RIGHT, R> ? 8 : 4;
+// right-view scatter: pair the two candidates of one u in registers (one ds_min per u) except where
+// the extra live values push the fused loop past 128 VGPRs (r = 3: NQ = 16)
+template <int R>
+constexpr bool kPairedScatter = (R != 3);
+template <bool RIGHT, int R>
+constexpr int kMinWavesPerEU = (RIGHT && !kWideRight<RIGHT, R>) ? 2 : 4;
 constexpr int kTileH = 32;
 constexpr int kPairs = 4;
 constexpr int kChunk = 2 * kPairs;
 constexpr int kCols = 64;
 
-template <int R, int DMAX>
+template <int R, int DMAX, int NW = 4>
 struct Geo {
     static constexpr int TW = kCols - 2 * R;                  // output columns per tile
     static constexpr int ROWS = kTileH + 2 * R;                 // input rows per tile
@@ -40,10 +55,13 @@ struct Geo {
     static constexpr int NQ = (((TW + 3) / 4) + 1) & ~1;        // outputs per phase-H thread (even: b64 reads)
     static constexpr int NCS2 = (NQ + 2 * R + 1) / 2;           // 8-B CS reads per phase-H thread
     static constexpr int NEED = 3 * NQ + 2 * NCS2;              // last CS column read + 1
-    // row stride in dwords == 4 (mod 64): the 32 lanes of a ds_read_b64 group (16 rows x 2
-    // quarters, quarter offsets NQ apart with NQ == 2 mod 4) start on 32 distinct even banks
-    static constexpr int CSS = ((NEED - 4 + 63) / 64) * 64 + 4;
-    static constexpr int CS_BYTES = 4 * HALF * CSS * 4;         // 4 waves x one half-tile plane
+    // row stride in dwords: for NQ == 2 (mod 4) a stride == 4 (mod 8) puts the 32 lanes of a
+    // ds_read_b64 group (16 rows x 2 quarters) on 64 distinct banks; for NQ == 16 no stride is
+    // conflict-free; the smallest even one that is not a multiple of 32 is 2-way
+    static constexpr int CSS_EVEN = (NEED + 1) & ~1;
+    static constexpr int CSS = (NQ % 4 == 2) ? (NEED + ((12 - NEED % 8) % 8))
+                                             : (CSS_EVEN % 32 == 0 ? CSS_EVEN + 2 : CSS_EVEN);
+    static constexpr int CS_BYTES = NW * HALF * CSS * 4;        // NW waves x one half-tile plane
     static constexpr int RW = kCols + DMAX + 4;                 // u16 entries per right-band row (x4-aligned base)
     static constexpr int NDW = RW / 4;                          // dwords staged per right-band row
     static constexpr int LSTR = kCols + 4;                      // bytes per staged left row
@@ -53,12 +71,18 @@ struct Geo {
     static constexpr int FRONT0 = CS_BYTES > FOLD_BYTES ? CS_BYTES : FOLD_BYTES;
     static constexpr int FRONT = ((FRONT0 > L_BYTES ? FRONT0 : L_BYTES) + 15) & ~15;  // CS / fold / L alias
     static constexpr int LDS_BYTES = FRONT + RS_BYTES;
+    // fused right view (RIGHT kernels): per-tile right-key rows indexed by u - (x0 - DMAX - 1);
+    // row stride == 1 (mod 64) keeps the 64 lanes of a scatter on distinct banks (2-way for NQ 14)
+    static constexpr int PW = TW + DMAX + 1;                    // partial row width written to HBM
+    static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
+    static constexpr int RB_BYTES = kTileH * RBW * 4;
+#if SM_ABLATE & 32
+    static constexpr int LDS_BYTES_R = LDS_BYTES;
+#else
+    static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
+#endif
     static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
 };
-
-__device__ __forceinline__ uint32_t ld_u8(const uint8_t* p, int y, int x, int W, int H, int pitch) {
-    return (y >= 0 && y < H && x >= 0 && x < W) ? (uint32_t)p[(int64_t)y * pitch + x] : 0u;
-}
 
 // 4 image bytes of row y from column x (little-endian), bytes outside the image read as 0.
 // Interior dwords are one (possibly unaligned) global_load_dword; border dwords go byte-wise.
@@ -86,13 +110,25 @@ __host__ __device__ constexpr uint32_t sel_a(int k) { return 0x0C0C0500u | (uint
 __host__ __device__ constexpr uint32_t sel_b(int k) { return 0x0C0C0004u | ((uint32_t)k << 8); }
 constexpr uint32_t kSelW = 0x0C0C0504u;
 
-template <int R, int DMAX>
-__global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
-    using G = Geo<R, DMAX>;
+// RIGHT = true additionally produces the right view (StereoHelper.cpp:156-180): its cost is
+// C_R(u, d) = C_L(u + d, d), so every key (S << 8 | d) formed for left pixel x is also a candidate
+// for right pixel u = x - d.  Phase H scatter-mins them into a per-tile LDS row (ds_min_u32) that
+// is written to `a.rpart`; right_reduce_lr_kernel folds the ~(TW + D) / TW tiles covering each u.
+// This replaces a second matching pass over the mirrored pair.
+template <int R, int DMAX, bool RIGHT>
+__global__ __launch_bounds__((64 * kWaves<RIGHT, R>), (kMinWavesPerEU<RIGHT, R>))
+void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
+    constexpr int NW = kWaves<RIGHT, R>;
+    constexpr int kThreads = 64 * NW;
+    using G = Geo<R, DMAX, NW>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [kPairs][kTileH][CSS]
+    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [NW][HALF][CSS]
     uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::FRONT);          // [ROWS][RW]
-    uint8_t* rsb = smem + G::FRONT;                                       // byte view of rs
+#if SM_ABLATE & 32
+    uint32_t* rb = reinterpret_cast<uint32_t*>(smem);
+#else
+    uint32_t* rb = reinterpret_cast<uint32_t*>(smem + G::FRONT + G::RS_BYTES);  // RIGHT: [kTileH][RBW]
+#endif
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -173,12 +209,16 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
         for (int o = 0; o < G::NQ; ++o) best[h][o] = a.seed_key;
 
     const int xmax_tile = min(x0 + G::TW, W) - 1;
-    const bool d_edge = a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0);
+    const bool d_edge = (a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0)) ||
+                        (RIGHT && x0 + G::TW > W);
     const bool col_in = (c >= 0) && (c < W);
     const int npairs = dspan >> 1;                 // multiple of 4
-    const int p_lo = (wave * npairs) / 4;
-    const int p_hi = ((wave + 1) * npairs) / 4;
+    const int p_lo = (wave * npairs) / NW;
+    const int p_hi = ((wave + 1) * npairs) / NW;
     uint32_t* csw = cs + wave * (G::HALF * G::CSS);   // this wave's private half-tile CS plane
+    if constexpr (RIGHT) {
+        for (int e = tid; e < kTileH * G::RBW; e += kThreads) rb[e] = 0xFFFFFFFFu;
+    }
 
     __syncthreads();   // lq reads of the aliased staging area are done before any CS write
 
@@ -231,6 +271,10 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
                 uint32_t S = 0u;
 #pragma unroll
                 for (int k = 0; k < 2 * R; ++k) S += v[k];
+                // RIGHT: klo of output o goes to u_o = x_o - d, khi to u_o - 1 = u_{o-1}; the two
+                // candidates of one u are min'ed in registers, one ds_min_u32 per u
+                uint32_t* rrow = rb + (h * G::HALF + hj) * G::RBW + (obase - d + DMAX + 1);   // + o: u_o
+                uint32_t plo = 0xFFFFFFFFu;
                 if (!dm) {
 #pragma unroll
                     for (int o = 0; o < G::NQ; ++o) {
@@ -238,6 +282,18 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
                         const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
                         const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
                         best[h][o] = min(best[h][o], min(klo, khi));
+                        if constexpr (RIGHT) {
+                            // outputs past TW (last quarter only) read CS columns outside the tile
+                            const bool ov = (o >= G::TW - 3 * G::NQ) && (obase + o >= G::TW);
+                            if constexpr (kPairedScatter<R>) {
+                                const uint32_t rhi = ov ? 0xFFFFFFFFu : khi;
+                                atomicMin(rrow + o - 1, min(plo, rhi));
+                                plo = ov ? 0xFFFFFFFFu : klo;
+                            } else if (!ov) {
+                                atomicMin(rrow + o - 1, khi);
+                                atomicMin(rrow + o, klo);
+                            }
+                        }
                         S -= v[o];
                     }
                 } else {
@@ -246,14 +302,27 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
                         S += v[o + 2 * R];
                         const int x = x0 + obase + o;
                         const int lim = a.valid_mode == 0 ? (W - x) : x;
-                        uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
-                        uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
-                        klo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
-                        khi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
-                        best[h][o] = min(best[h][o], min(klo, khi));
+                        const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                        const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                        const uint32_t mlo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
+                        const uint32_t mhi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
+                        best[h][o] = min(best[h][o], min(mlo, mhi));
+                        if constexpr (RIGHT) {
+                            const bool okx = (obase + o < G::TW) && (x < W);
+                            const uint32_t rhi = (okx && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
+                            const uint32_t rlo = (okx && d < d_hi) ? klo : 0xFFFFFFFFu;
+                            if constexpr (kPairedScatter<R>) {
+                                atomicMin(rrow + o - 1, min(plo, rhi));
+                                plo = rlo;
+                            } else {
+                                atomicMin(rrow + o - 1, rhi);
+                                atomicMin(rrow + o, rlo);
+                            }
+                        }
                         S -= v[o];
                     }
                 }
+                if constexpr (RIGHT && kPairedScatter<R>) atomicMin(rrow + G::NQ - 1, plo);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -265,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
 #if SM_ABLATE & 4
     if (a.W > 0) { if (tid == 0) a.disp[0] = (uint8_t)(best[0][0] ^ best[1][G::NQ - 1]); return; }
 #endif
-    // ---- fold the 4 waves (same lane = same pixels in every wave) through one LDS plane ----
+    // ---- fold the NW waves (same lane = same pixels in every wave) through one LDS plane ----
     uint32_t* fold = cs;                                   // [kTileH][TW] keys
     if (wave == 0) {
 #pragma unroll
@@ -293,26 +362,102 @@ __global__ __launch_bounds__(kThreads, 4) void box_match_kernel(MatchArgs a, int
         if (Df) Df[(int64_t)y * a.out_pitch + x] = k < a.thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
         if (Kf) Kf[(int64_t)y * W + x] = k;
     }
+    if constexpr (RIGHT) {
+        // rb is untouched by the fold (which aliases the CS area); rows past H are never read
+        uint32_t* P = a.rpart + (int64_t)blockIdx.x * (kTileH * G::PW);   // [frame][ty][tx][kTileH][PW]
+        for (int e = tid; e < kTileH * G::PW; e += kThreads) {
+            const int j = e / G::PW;
+            P[e] = rb[j * G::RBW + (e - j * G::PW)];
+        }
+    }
 }
 
-template <int R, int DMAX>
-hipError_t launch_rd(const MatchArgs& a, int batch, hipStream_t s) {
-    using G = Geo<R, DMAX>;
+// Right view + LR check for one image row per block.  Right key of u = min over the tiles whose
+// partial rows cover u (x0 - DMAX - 1 <= u < x0 + TW, x0 <= u + d_hi - 1); dR = key & 0xFF with no
+// threshold (StereoHelper.cpp:131-154).  Then StereoDisparity.cpp:136-147 on the row:
+//   d = dL(x); occ = x-d < 0 || d == 0 || |d - dR(x-d)| > 1;  out = occ ? 0 : d.
+__global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
+                                                              int tiles_y, int TW, int PW, int dmax, int d_hi, int W,
+                                                              int H, uint8_t* disp, int opitch, int64_t ostride,
+                                                              uint8_t* __restrict__ right_out,
+                                                              uint8_t* __restrict__ mask_out, int apitch,
+                                                              int64_t astride) {
+    extern __shared__ uint8_t dr_row[];
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int ty = y / kTileH, j = y - ty * kTileH;
+    const uint32_t* base = rpart + (((int64_t)f * tiles_y + ty) * tiles_x * kTileH + j) * PW;
+    const int64_t tstride = (int64_t)kTileH * PW;
+    uint8_t* rrow = right_out ? right_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    for (int u = threadIdx.x; u < W; u += blockDim.x) {
+        const int tlo = u / TW;
+        const int thi = min(tiles_x - 1, (u + d_hi - 1) / TW);
+        uint32_t key = 0xFFFFFFFFu;
+        for (int tx = tlo; tx <= thi; ++tx) key = min(key, base[tx * tstride + (u - tx * TW + dmax + 1)]);
+        const uint8_t dr = (uint8_t)(key & 0xFFu);
+        dr_row[u] = dr;
+        if (rrow) rrow[u] = dr;
+    }
+    __syncthreads();
+    uint8_t* drow = disp + (int64_t)f * ostride + (int64_t)y * opitch;
+    uint8_t* mrow = mask_out ? mask_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        const int d = drow[x];
+        int occ = 1;
+        if (x - d >= 0) {
+            const int diff = d - (int)dr_row[x - d];
+            occ = (d == 0) || diff > 1 || diff < -1;
+        }
+        drow[x] = occ ? (uint8_t)0 : (uint8_t)d;
+        if (mrow) mrow[x] = (uint8_t)!occ;
+    }
+}
+
+// Output buffers of the fused right view (launch_box_match_lr).
+struct RightOut {
+    uint8_t* right;   // optional dR
+    uint8_t* mask;    // optional valid mask
+    int pitch;
+    int64_t stride;
+};
+
+template <int R, int DMAX, bool RIGHT>
+hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStream_t s) {
+    using G = Geo<R, DMAX, kWaves<RIGHT, R>>;
     const int tiles_x = (a.W + G::TW - 1) / G::TW;
     const int tiles_y = (a.H + kTileH - 1) / kTileH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((box_match_kernel<R, DMAX>), dim3((unsigned)blocks), dim3(kThreads), (size_t)G::LDS_BYTES, s,
-                       a, tiles_x, tiles_y);
+    if constexpr (RIGHT) {
+        hipLaunchKernelGGL((box_match_kernel<R, DMAX, true>), dim3((unsigned)blocks), dim3(64 * kWaves<true, R>),
+                           (size_t)G::LDS_BYTES_R, s, a, tiles_x, tiles_y);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(right_reduce_lr_kernel, dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart, tiles_x,
+                           tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, a.disp, a.out_pitch, a.out_frame_stride,
+                           ro->right, ro->mask, ro->pitch, ro->stride);
+    } else {
+        hipLaunchKernelGGL((box_match_kernel<R, DMAX, false>), dim3((unsigned)blocks), dim3(64 * kWaves<false, R>),
+                           (size_t)G::LDS_BYTES, s, a, tiles_x, tiles_y);
+    }
     return hipGetLastError();
 }
 
-template <int R>
-hipError_t launch_r(const MatchArgs& a, int batch, hipStream_t s) {
+template <int R, bool RIGHT>
+hipError_t launch_r(const MatchArgs& a, int batch, const RightOut* ro, hipStream_t s) {
     const int dspan = (a.d_hi - a.d_lo + kChunk - 1) & ~(kChunk - 1);
-    if (dspan <= 64) return launch_rd<R, 64>(a, batch, s);
-    if (dspan <= 128) return launch_rd<R, 128>(a, batch, s);
-    return launch_rd<R, 256>(a, batch, s);
+    if (dspan <= 64) return launch_rd<R, 64, RIGHT>(a, batch, ro, s);
+    if (dspan <= 128) return launch_rd<R, 128, RIGHT>(a, batch, ro, s);
+    return launch_rd<R, 256, RIGHT>(a, batch, ro, s);
+}
+
+template <int R>
+size_t partial_bytes_r(int W, int H, int D, int batch) {
+    const int dspan = (D + kChunk - 1) & ~(kChunk - 1);
+    const int dmax = dspan <= 64 ? 64 : (dspan <= 128 ? 128 : 256);
+    const int TW = kCols - 2 * R;
+    const int PW = TW + dmax + 1;
+    const size_t tiles = (size_t)((W + TW - 1) / TW) * ((H + kTileH - 1) / kTileH);
+    return tiles * (size_t)batch * kTileH * PW * 4;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -358,15 +503,46 @@ __global__ __launch_bounds__(256) void box_match_generic_kernel(MatchArgs a, int
 
 hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s) {
     switch (a.radius) {
-        case 0: return launch_r<0>(a, batch, s);
-        case 1: return launch_r<1>(a, batch, s);
-        case 2: return launch_r<2>(a, batch, s);
-        case 3: return launch_r<3>(a, batch, s);
-        case 4: return launch_r<4>(a, batch, s);
-        case 5: return launch_r<5>(a, batch, s);
-        case 6: return launch_r<6>(a, batch, s);
-        case 7: return launch_r<7>(a, batch, s);
+        case 0: return launch_r<0, false>(a, batch, nullptr, s);
+        case 1: return launch_r<1, false>(a, batch, nullptr, s);
+        case 2: return launch_r<2, false>(a, batch, nullptr, s);
+        case 3: return launch_r<3, false>(a, batch, nullptr, s);
+        case 4: return launch_r<4, false>(a, batch, nullptr, s);
+        case 5: return launch_r<5, false>(a, batch, nullptr, s);
+        case 6: return launch_r<6, false>(a, batch, nullptr, s);
+        case 7: return launch_r<7, false>(a, batch, nullptr, s);
         default: return launch_box_match_generic(a, batch, s);
+    }
+}
+
+size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch) {
+    switch (radius) {
+        case 0: return partial_bytes_r<0>(W, H, D, batch);
+        case 1: return partial_bytes_r<1>(W, H, D, batch);
+        case 2: return partial_bytes_r<2>(W, H, D, batch);
+        case 3: return partial_bytes_r<3>(W, H, D, batch);
+        case 4: return partial_bytes_r<4>(W, H, D, batch);
+        case 5: return partial_bytes_r<5>(W, H, D, batch);
+        case 6: return partial_bytes_r<6>(W, H, D, batch);
+        case 7: return partial_bytes_r<7>(W, H, D, batch);
+        default: return 0;
+    }
+}
+
+hipError_t launch_box_match_lr(const MatchArgs& a, int batch, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
+                               int64_t aux_stride, hipStream_t s) {
+    if (a.d_lo != 0 || a.valid_mode != 0 || !a.disp || !a.rpart) return hipErrorInvalidValue;
+    const RightOut ro{right_out, mask_out, aux_pitch, aux_stride};
+    switch (a.radius) {
+        case 0: return launch_r<0, true>(a, batch, &ro, s);
+        case 1: return launch_r<1, true>(a, batch, &ro, s);
+        case 2: return launch_r<2, true>(a, batch, &ro, s);
+        case 3: return launch_r<3, true>(a, batch, &ro, s);
+        case 4: return launch_r<4, true>(a, batch, &ro, s);
+        case 5: return launch_r<5, true>(a, batch, &ro, s);
+        case 6: return launch_r<6, true>(a, batch, &ro, s);
+        case 7: return launch_r<7, true>(a, batch, &ro, s);
+        default: return hipErrorInvalidValue;
     }
 }
 

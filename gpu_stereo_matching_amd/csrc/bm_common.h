@@ -20,6 +20,7 @@ struct MatchArgs {
     int out_pitch;
     int64_t out_frame_stride;
     uint32_t* keys;         // optional: packed keys [batch][H][W] (multi-GPU slice reduction)
+    uint32_t* rpart;        // fused right view: per-tile right-key partials (box_right_partial_bytes)
 };
 
 constexpr int kMaxDisp = 256;      // uint8 output / 8-bit d field of the packed key
@@ -28,6 +29,11 @@ constexpr int kMaxFastRadius = 7;  // u16 packed sums stay < 2^16 up to r = 7 (1
 // Host-side launchers (bm_box.hip, bm_aux.hip).
 hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s);
 hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s);
+// Box matching + right view + LR check in two launches (radius <= kMaxFastRadius, d_lo == 0):
+// a.disp receives the checked left disparity, right_out/mask_out (optional) dR and the valid mask.
+hipError_t launch_box_match_lr(const MatchArgs& a, int batch, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
+                               int64_t aux_stride, hipStream_t s);
+size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch);
 hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key,
                                uint8_t* disp, int out_pitch, hipStream_t s);
 hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch,

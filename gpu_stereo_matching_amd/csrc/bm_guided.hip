@@ -141,7 +141,6 @@ __global__ __launch_bounds__(kT, 2) void guided_ab_kernel(const uint8_t* __restr
     }
     // phase-H ownership: row hj, half hh -> outputs [hh*NOUT, hh*NOUT + NOUT)
     const int hj = lane & 31, hh = lane >> 5, obase = hh * G::NOUT;
-    const int yo = y0 + hj;
     // per-pixel d-independent constants in LDS: {N, SI, 1/(N^2 var + eps N^2), 1/N}
     for (int e = tid; e < kABRows * G::TW; e += kT) {
         const int i = e / G::TW, j = e % G::TW;

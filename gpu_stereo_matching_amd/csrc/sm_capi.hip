@@ -28,6 +28,9 @@ struct sm_handle {
     // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
     uint8_t* d_lr = nullptr;
     size_t lr_bytes = 0;
+    // fused right view: per-tile right-key partials (grown on demand)
+    uint32_t* d_rpart = nullptr;
+    size_t rpart_bytes = 0;
     // BGR staging for sm_block_match_bgr_u8 (grown on demand)
     uint8_t* d_bgr = nullptr;
     size_t bgr_bytes = 0;
@@ -86,6 +89,16 @@ int ensure_lr(sm_handle* h, size_t bytes) {
     return SM_OK;
 }
 
+int ensure_rpart(sm_handle* h, size_t bytes) {
+    if (h->rpart_bytes >= bytes) return SM_OK;
+    if (h->d_rpart) (void)hipFree(h->d_rpart);
+    h->d_rpart = nullptr;
+    h->rpart_bytes = 0;
+    SM_HIP(hipMalloc(&h->d_rpart, bytes));
+    h->rpart_bytes = bytes;
+    return SM_OK;
+}
+
 // Core device-side pass over `batch` frames.
 int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
@@ -132,8 +145,20 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     a.out_pitch = opitch;
     a.out_frame_stride = ostride;
     a.keys = nullptr;
+    a.rpart = nullptr;
+    if (!lr) {
+        SM_HIP(sm::launch_box_match(a, batch, s));
+        return SM_OK;
+    }
+    if (radius <= sm::kMaxFastRadius) {
+        // right view fused into the matching pass (C_R(u,d) = C_L(u+d,d), StereoHelper.cpp:156-180)
+        int rc = ensure_rpart(h, sm::box_right_partial_bytes(W, H, radius, D, batch));
+        if (rc) return rc;
+        a.rpart = h->d_rpart;
+        SM_HIP(sm::launch_box_match_lr(a, batch, right_out, mask_out, apitch, astride, s));
+        return SM_OK;
+    }
     SM_HIP(sm::launch_box_match(a, batch, s));
-    if (!lr) return SM_OK;
 
     // Right view (StereoHelper.cpp:156-180 + :131-154) as the left matcher on the mirrored pair,
     // validity d <= x (mirrored) and no threshold; then the StereoDisparity.cpp:136-147 check.
@@ -259,6 +284,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_right);
     (void)hipFree(h->d_disp);
     (void)hipFree(h->d_lr);
+    (void)hipFree(h->d_rpart);
     (void)hipFree(h->d_bgr);
     sm::guided_workspace_free(h->gws);
     for (auto& ev : h->ev)

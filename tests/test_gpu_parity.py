@@ -160,12 +160,36 @@ def test_lr_golden(matcher, gray, bm_expected):
         assert np.array_equal(chk2, chk)
 
 
-@pytest.mark.parametrize("r,D", [(1, 16), (4, 64), (5, 128)])
+@pytest.mark.parametrize("r,D", [(0, 8), (1, 16), (2, 1), (3, 37), (4, 64), (5, 128), (6, 256), (7, 100), (8, 48),
+                                 (5, 2), (5, 129)])
 def test_lr_random(matcher, oracle, r, D):
+    """r <= 7: right view fused into the matching pass (rpart + reduce); r = 8: mirrored second pass."""
     L, R = oracle.synth_pair(r * 7 + D, 257, 61, max(D, 16))
     disp, rd, chk, mask = oracle.box_lr(L, R, r, D)
     c, rr, mm = matcher.match_lr(L, R, r, D)
-    assert np.array_equal(rr, rd) and np.array_equal(c, chk) and np.array_equal(mm, mask)
+    assert np.array_equal(rr, rd), (r, D)
+    assert np.array_equal(c, chk) and np.array_equal(mm, mask), (r, D)
+
+
+@pytest.mark.parametrize("W,H,r,D", [(40, 30, 3, 64), (53, 7, 5, 64), (3, 5, 1, 8), (1000, 33, 5, 256), (600, 97, 7, 192)])
+def test_lr_shapes(matcher, oracle, W, H, r, D):
+    """Narrow (W < TW, W < D), single-tile, ragged and tall shapes through the fused right view."""
+    L, R = oracle.synth_pair(W * 3 + H, W, H, max(D, 16))
+    disp, rd, chk, mask = oracle.box_lr(L, R, r, D)
+    c, rr, mm = matcher.match_lr(L, R, r, D)
+    assert np.array_equal(rr, rd) and np.array_equal(c, chk) and np.array_equal(mm, mask), (W, H, r, D)
+
+
+def test_lr_device_batch(matcher, oracle, torch):
+    W, H, D, r, B = 301, 70, 64, 4, 3
+    pairs = [oracle.synth_pair(900 + b, W, H, D) for b in range(B)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D, lr_check=True)
+    torch.cuda.synchronize()
+    for b in range(B):
+        _, _, chk, _ = oracle.box_lr(pairs[b][0], pairs[b][1], r, D)
+        assert np.array_equal(out[b].cpu().numpy(), chk), b
 
 
 @pytest.mark.parametrize("cuts", [[0, 128], [0, 64, 128], [0, 16, 32, 48, 64, 80, 96, 112, 128], [0, 5, 77, 128]])

@@ -9,10 +9,12 @@ m = sm.BlockMatcher(0, 1920, 1080, 256)
 pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(4)]
 Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda(); Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
 out = torch.empty_like(Lt)
-for _ in range(5): m.match_device(Lt, Rt, 5, 128, out_t=out)
+LR = bool(int(os.environ.get('SM_AB_LR', '0')))
+RAD = int(os.environ.get('SM_AB_R', '5'))
+for _ in range(5): m.match_device(Lt, Rt, RAD, 128, out_t=out, lr_check=LR)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-for _ in range(40): m.match_device(Lt, Rt, 5, 128, out_t=out)
+for _ in range(40): m.match_device(Lt, Rt, RAD, 128, out_t=out, lr_check=LR)
 e1.record(); torch.cuda.synchronize()
 print(sys.argv[1], "ms/frame", e0.elapsed_time(e1) / 40 / 4)
