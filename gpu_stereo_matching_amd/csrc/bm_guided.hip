@@ -350,7 +350,7 @@ struct GeoF {
 };
 
 template <int R>
-__global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ Rimg,
+__global__ __launch_bounds__(kT, ((R == 3 || R == 7) ? 2 : 3)) void guided_fused_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ Rimg,
                                                              int W, int H, int pitch, int D, float eps, int valid_mode,
                                                              uint8_t* __restrict__ disp, int out_pitch, int tiles_x) {
     using G = GeoF<R>;
@@ -396,9 +396,9 @@ __global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __re
     const int c = lane;
     const int xc = px0 + c;
     const bool col_in = xc >= 0 && xc < W;
-    uint32_t lz[G::NV];
+    uint32_t lzm[G::NV];   // (L << 12) | 1: the S1V multiplier; L itself is lzm >> 12
 #pragma unroll
-    for (int t = 0; t < G::NV; ++t) lz[t] = (a0 + t < G::PH) ? (uint32_t)lt[(a0 + t) * 64 + c] : 0u;
+    for (int t = 0; t < G::NV; ++t) lzm[t] = (((a0 + t < G::PH) ? (uint32_t)lt[(a0 + t) * 64 + c] : 0u) << 12) | 1u;
     __syncthreads();   // lt (aliased with cs) is consumed
 
     // S1H ownership: A row h1i, segment h1s (threads >= AH*NSEG1 idle in S1H)
@@ -415,15 +415,16 @@ __global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __re
     // per-A-pixel constants (filled by the stats pass) and per-output WTA state
     uint32_t nN[G::SW1], nSI[G::SW1];
     float invden[G::SW1], invN[G::SW1];
-    float oI[G::SW2], oinvN[G::SW2], bq[G::SW2];
+    // WTA on N*q = sum(a)*I + sum(b) (N = output window count > 0 is constant per pixel, so the
+    // argmin is that of q); the Device.cu:37 seed 50 becomes 50*N (exact in fp32)
+    float oI[G::SW2], bq[G::SW2];
     int bdd[G::SW2];
 #pragma unroll
     for (int o = 0; o < G::SW2; ++o) {
         const int x = x0 + h2s * G::SW2 + o;
         const bool ok = oy < H && x < W && h2s * G::SW2 + o < G::TW;
         oI[o] = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
-        oinvN[o] = ok ? 1.0f / (float)(win_count(x, R, W) * win_count(oy, R, H)) : 0.f;
-        bq[o] = valid_mode == 0 ? 50.0f : __builtin_huge_valf();
+        bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
     }
 
@@ -437,9 +438,9 @@ __global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __re
             for (int t = 0; t < G::NV; ++t) {
                 const int i = a0 + t;                                   // P row
                 const uint32_t rv = (d < 0 || i >= G::PH) ? 0u : (uint32_t)rc[i * G::RBW];
-                uint32_t ad = __builtin_amdgcn_sad_u8(lz[t], rv, 0u);
+                uint32_t ad = __builtin_amdgcn_sad_u8(lzm[t] >> 12, rv, 0u);
                 ad = m ? ad : 0u;
-                T += __umul24(ad, (lz[t] << 12) | 1u);
+                T = __umul24(ad, lzm[t]) + T;
                 if (t >= 2 * R) {
                     const uint32_t old = (t == 2 * R) ? 0u : Tp[(t - 2 * R - 1) % (2 * R + 1)];
                     const int j = i - 2 * R;                            // A row
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(kT, 2) void guided_fused_kernel(const uint8_t* __re
                 const float2 vin = row[o + 2 * R];
                 sa += vin.x;
                 sb += vin.y;
-                const float q = (sa * oI[o] + sb) * oinvN[o];
+                const float q = sa * oI[o] + sb;
                 const int x = x0 + h2s * G::SW2 + o;
                 const int lim = valid_mode == 0 ? (W - x) : x;
                 if (d <= lim && q < bq[o]) {
