@@ -34,8 +34,6 @@ struct sm_handle {
     // BGR staging for sm_block_match_bgr_u8 (grown on demand)
     uint8_t* d_bgr = nullptr;
     size_t bgr_bytes = 0;
-    // guided workspace
-    sm::GuidedWorkspace gws;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float stage_ms[3] = {0.f, 0.f, 0.f};
@@ -114,17 +112,17 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
             uint8_t* mL = h->d_lr;
             uint8_t* mR = mL + P * batch;
             uint8_t* rdm = mR + P * batch;
-            SM_HIP(sm::launch_guided_match(h->gws, L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0,
+            SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0,
                                           disp, opitch, ostride, s));
             SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
             SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
-            SM_HIP(sm::launch_guided_match(h->gws, mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, rdm, W,
+            SM_HIP(sm::launch_guided_match(mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, rdm, W,
                                           P, s));
             SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rdm, W, P, W, H, batch, disp, opitch, ostride,
                                        right_out, mask_out, apitch, astride, s));
             return SM_OK;
         }
-        SM_HIP(sm::launch_guided_match(h->gws, L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, disp,
+        SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, disp,
                                       opitch, ostride, s));
         return SM_OK;
     }
@@ -286,7 +284,6 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_lr);
     (void)hipFree(h->d_rpart);
     (void)hipFree(h->d_bgr);
-    sm::guided_workspace_free(h->gws);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);

@@ -13,10 +13,11 @@ LR = bool(int(os.environ.get('SM_AB_LR', '0')))
 RAD = int(os.environ.get('SM_AB_R', '5'))
 AGG = os.environ.get('SM_AB_AGG', 'box')
 NIT = 40 if AGG == 'box' else 5
-for _ in range(2 if AGG != 'box' else 5): m.match_device(Lt, Rt, RAD, 128, out_t=out, lr_check=LR, agg=AGG)
+DD = int(os.environ.get('SM_AB_D', '128'))
+for _ in range(2 if AGG != 'box' else 5): m.match_device(Lt, Rt, RAD, DD, out_t=out, lr_check=LR, agg=AGG)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-for _ in range(NIT): m.match_device(Lt, Rt, RAD, 128, out_t=out, lr_check=LR, agg=AGG)
+for _ in range(NIT): m.match_device(Lt, Rt, RAD, DD, out_t=out, lr_check=LR, agg=AGG)
 e1.record(); torch.cuda.synchronize()
 print(sys.argv[1], "ms/frame", e0.elapsed_time(e1) / NIT / 4)
