@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=4, help="frames per step per GPU")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the per-config / LR / guided table")
+    ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--profile", action="store_true",
+                    help="only the timed steps (what rocprof summaries under profiles/ are taken from)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_box_r5_1080p.json"))
     return ap.parse_args()
 
@@ -72,8 +75,55 @@ def cpu_baseline(W, H, D, r, seed):
                       f"{dt:.2f} s/map"}
 
 
+# BASELINE.json configs measured next to the headline (rank 0, device-resident synthetic pairs,
+# `batch` frames per call).  cfg1/cfg2 are quoted on the bundled Middlebury pairs; the bench uses
+# synthetic pairs of the same size because /root/reference is not on the GPU box.
+VARIANTS = (
+    # name, W, H, D, r, agg, lr, batch
+    ("cfg1 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, 16),
+    ("cfg2 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, 16),
+    ("cfg3 1080p 11x11 box+lr d128", 1920, 1080, 128, 5, "box", True, 4),
+    ("cfg3 1080p 11x11 guided d128", 1920, 1080, 128, 5, "guided", False, 4),
+    ("cfg3 1080p 11x11 guided+lr d128", 1920, 1080, 128, 5, "guided", True, 4),
+    ("cfg4 1080p 11x11 box d256", 1920, 1080, 256, 5, "box", False, 4),
+    ("cfg5 4K 11x11 box d192", 3840, 2160, 192, 5, "box", False, 2),
+    ("cfg5 4K 11x11 box+lr d192", 3840, 2160, 192, 5, "box", True, 2),
+    ("cfg5 4K 11x11 guided+lr d192", 3840, 2160, 192, 5, "guided", True, 2),
+)
+
+
+def run_variants(sm, torch, dev, stream, seed):
+    out = {}
+    m = sm.BlockMatcher(dev.index, 3840, 2160, 256)
+    try:
+        for (name, W, H, D, r, agg, lr, B) in VARIANTS:
+            try:
+                pairs = [sm.synth_pair(seed + i, W, H, D) for i in range(B)]
+                Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
+                Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
+                o = torch.empty_like(Lt)
+                for _ in range(2):
+                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, stream=stream)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                nrep = 10 if agg == "box" else 3
+                e0.record(stream)
+                for _ in range(nrep):
+                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, stream=stream)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms = e0.elapsed_time(e1) / (nrep * B)
+                out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": B}
+            except Exception as e:  # report, never hide
+                out[name] = {"error": str(e)}
+    finally:
+        m.close()
+    return out
+
+
 def main():
     args = parse()
+    if args.profile:
+        args.no_cpu_baseline = args.no_variants = args.no_latency = True
     import torch
     import torch.distributed as dist
 
@@ -137,7 +187,7 @@ def main():
 
     # ---- single-frame latency (batch 1, device resident) ----
     lat = None
-    if rank == 0:
+    if rank == 0 and not args.no_latency:
         o1 = torch.empty_like(Lt[0])
         for _ in range(5):
             m.match_device(Lt[0], Rt[0], r, D, out_t=o1, stream=stream)
@@ -175,27 +225,10 @@ def main():
                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": "all_reduce MIN int32 (RCCL)",
                   "keys_bytes_per_frame": W * H * 4, "scaling": "strong"}
 
-    # ---- variants on rank 0 (LR check) ----
+    # ---- BASELINE configs, LR and guided variants on rank 0 ----
     variants = None
     if rank == 0 and not args.no_variants:
-        variants = {}
-        o1 = torch.empty_like(Lt[0])
-        for name, kw in (("box+lr", dict(lr_check=True)), ("guided", dict(agg="guided")),
-                         ("guided+lr", dict(agg="guided", lr_check=True))):
-            try:
-                for _ in range(3):
-                    m.match_device(Lt[0], Rt[0], r, D, out_t=o1, stream=stream, **kw)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                nrep = 20 if "guided" not in name else 5
-                for _ in range(nrep):
-                    m.match_device(Lt[0], Rt[0], r, D, out_t=o1, stream=stream, **kw)
-                e1.record(stream)
-                torch.cuda.synchronize(dev)
-                ms = e0.elapsed_time(e1) / nrep
-                variants[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000 / ms, 2)}
-            except Exception as e:  # report, never hide
-                variants[name] = {"error": str(e)}
+        variants = run_variants(sm, torch, dev, stream, args.seed)
 
     if rank == 0:
         bpm = algorithmic_bytes_per_map(W, H, D)

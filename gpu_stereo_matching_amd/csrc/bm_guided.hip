@@ -52,7 +52,9 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t* p, int y, int x, int W, i
     return v;
 }
 
-template <int R, int DMAX>
+constexpr int kBandChunk = 64;   // disparities per staged right band
+
+template <int R>
 struct GeoF {
     static constexpr int TW = 64 - 4 * R;
     static constexpr int TH = 32;
@@ -65,14 +67,14 @@ struct GeoF {
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
     static constexpr int CSS0 = (NSEG1 * SW1 + 2 * R) > 64 ? (NSEG1 * SW1 + 2 * R) : 64;
-    // strides kept minimal so that r <= 5 with d_max <= 128 fits 3 workgroups per CU (<= 52 KB):
+    // strides kept minimal so that r <= 5 fits 3 workgroups per CU (<= 52 KB):
     // an odd CS stride spreads the S1H rows over the banks; S2H threads whose last outputs fall
     // past TW read beyond their mm row (the next row, or abp after the last one) into values
     // that only reach those discarded outputs
     static constexpr int CSS = CSS0 + 1;                     // u32 per CS row
     static constexpr int MS = AW;                            // float2 per mm row
     static constexpr int ABS = AW;                           // float2 per a/b row
-    static constexpr int RBW = 64 + DMAX;                    // right band bytes per P row
+    static constexpr int RBW = 64 + kBandChunk;              // right band bytes per P row (one d-chunk)
     static constexpr int CS_BYTES = ((AH * CSS * 4 > PH * 64 ? AH * CSS * 4 : PH * 64) + 15) & ~15;  // lt aliases cs
     static constexpr int MM_BYTES = TH * MS * 8;
     static constexpr int AB_BYTES = AH * ABS * 8;
@@ -80,16 +82,16 @@ struct GeoF {
     static constexpr int LDS = CS_BYTES + MM_BYTES + AB_BYTES + RB_BYTES;
 };
 
-// r = 7 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere
+// r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere
 template <int R>
-constexpr int kGuidedWavesPerEU = (R == 7) ? 2 : 3;
+constexpr int kGuidedWavesPerEU = (R >= 6) ? 2 : 3;
 
-template <int R, int DMAX>
+template <int R>
 __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride, int tiles_x,
     int tiles) {
-    using G = GeoF<R, DMAX>;
+    using G = GeoF<R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AH][CSS] packed sums
     uint8_t* lt = smem;                                                                 // [PH][64] (aliases cs)
@@ -103,15 +105,19 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
     const int x0 = tx * G::TW, y0 = ty * G::TH;
     const int px0 = x0 - 2 * R, py0 = y0 - 2 * R;      // P region origin (image coords)
-    const int rbase = px0 - DMAX;                     // image column of rb[.][0]
     const uint8_t* L = Limg + (int64_t)frame * fstride;
     const uint8_t* Rf = Rimg + (int64_t)frame * fstride;
 
-    // ---- stage right band (all d) and left P tile ----
-    for (int e = tid; e < G::PH * (G::RBW / 4); e += kT) {
-        const int i = e / (G::RBW / 4), j = e - (e / (G::RBW / 4)) * (G::RBW / 4);
-        *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = ld4(Rf, py0 + i, rbase + 4 * j, W, H, pitch);
-    }
+    // ---- right band of d-chunk k: rb[i][j] = R(py0 + i, px0 - 64k - 64 + j), so P column c at
+    //      disparity d (in chunk k) reads rb[i][c + 64 - (d & 63)] ----
+    auto stage_band = [&](int k) {
+        const int rbase = px0 - kBandChunk * k - kBandChunk;
+        for (int e = tid; e < G::PH * (G::RBW / 4); e += kT) {
+            const int i = e / (G::RBW / 4), j = e - (e / (G::RBW / 4)) * (G::RBW / 4);
+            *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = ld4(Rf, py0 + i, rbase + 4 * j, W, H, pitch);
+        }
+    };
+    stage_band(0);
     for (int e = tid; e < G::PH * 16; e += kT) {
         const int i = e >> 4, j = e & 15;
         *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = ld4(L, py0 + i, px0 + 4 * j, W, H, pitch);
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     // ================= S1V: d < 0 is the guide-statistics pass (AD := L) =================
     auto s1v = [&](int d) {
         const bool m = d < 0 ? true : (col_in && xc >= d);
-        const uint8_t* rc = rb + (c - (d < 0 ? 0 : d) + DMAX);
+        const uint8_t* rc = rb + (c + kBandChunk - (d < 0 ? 0 : (d & (kBandChunk - 1))));
         uint32_t T = 0u, Tp[2 * R + 1];
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) {
@@ -267,11 +273,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     s1h(-1);
     __syncthreads();
     // buffers: cs (S1V -> S1H), abp (S1H -> S2V), mm (S2V -> S2H); each producer of iteration d+1
-    // runs after the barrier that ends the consumer of iteration d
+    // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
+    // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
     for (int d = 0; d <= D; ++d) {
         if (d < D) s1v(d);
         if (d > 0) s2v();
         __syncthreads();
+        if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
         if (d < D) s1h(d);
         if (d > 0) s2h(d - 1);
         __syncthreads();
@@ -285,26 +293,16 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     }
 }
 
-template <int R, int DMAX>
+template <int R>
 hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch,
                      int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride, hipStream_t s) {
-    using G = GeoF<R, DMAX>;
+    using G = GeoF<R>;
     const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((guided_fused_kernel<R, DMAX>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg, W,
+    hipLaunchKernelGGL((guided_fused_kernel<R>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg, W,
                        H, pitch, fstride, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y);
     return hipGetLastError();
-}
-
-template <int R>
-hipError_t run_r(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch, int D,
-                 float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride, hipStream_t s) {
-    if (D <= 64)
-        return run_fused<R, 64>(L, Rimg, W, H, pitch, fstride, batch, D, eps, valid_mode, disp, out_pitch, ostride, s);
-    if (D <= 128)
-        return run_fused<R, 128>(L, Rimg, W, H, pitch, fstride, batch, D, eps, valid_mode, disp, out_pitch, ostride, s);
-    return run_fused<R, 256>(L, Rimg, W, H, pitch, fstride, batch, D, eps, valid_mode, disp, out_pitch, ostride, s);
 }
 
 }  // namespace
@@ -314,7 +312,7 @@ hipError_t launch_guided_match(const uint8_t* L, const uint8_t* R, int W, int H,
                                int out_pitch, int64_t out_frame_stride, hipStream_t s) {
     if (D < 1 || D > kMaxDisp) return hipErrorInvalidValue;
 #define SM_GUIDED_CASE(r) \
-    case r: return run_r<r>(L, R, W, H, pitch, frame_stride, batch, D, eps, valid_mode, disp, out_pitch, out_frame_stride, s)
+    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, D, eps, valid_mode, disp, out_pitch, out_frame_stride, s)
     switch (radius) {
         SM_GUIDED_CASE(0);
         SM_GUIDED_CASE(1);
