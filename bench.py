@@ -10,9 +10,10 @@ that are already resident in HBM when the timed region starts.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Multi-GPU: one process per GPU.  The path partitions by frame (independent pairs), so ranks
-shard frames with no data-path collective ("scaling": "weak").  The d-slice mode of SURVEY §8e
-(each rank owns a disparity slice of the SAME frame, packed-key MIN all-reduce over RCCL) is
-measured in the same run for N > 1 and reported under "dslice".
+shard frames with no data-path collective ("scaling": "weak").  The two single-frame modes of
+SURVEY §8e are measured in the same run for N > 1: "dslice" (each rank owns a disparity slice of
+the SAME frame, packed-key MIN all-reduce over RCCL) and "rowband" (each rank owns a band of rows
+plus an r-row halo, all-gather of the uint8 bands).
 
 Rank 0 prints ONE JSON line.  Timing: barrier + synchronize on both sides of exactly K steps,
 max over ranks.  The dominant kernel's duration is measured live with HIP events on the stream
@@ -200,7 +201,7 @@ def main():
         lat = e0.elapsed_time(e1) / 50
 
     # ---- d-slice sharding of one frame with an RCCL MIN all-reduce (N > 1) ----
-    dslice = None
+    dslice = rowband = None
     if distributed:
         from gpu_stereo_matching_amd import sharding
         keys = torch.empty((H, W), dtype=torch.int32, device=dev)
@@ -224,6 +225,25 @@ def main():
         dslice = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": "all_reduce MIN int32 (RCCL)",
                   "keys_bytes_per_frame": W * H * 4, "scaling": "strong"}
+
+        # row bands of one frame (r-row halo, all-gather of uint8 bands)
+        def bstep():
+            sharding.match_rowband(m, Lt[0], Rt[0], r, D, rank, world, out_t=d1, stream=stream)
+
+        for _ in range(5):
+            bstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(n):
+            bstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        rowband = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
+                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": "all_gather uint8 bands (RCCL)",
+                   "halo_rows": r, "scaling": "strong"}
 
     # ---- BASELINE configs, LR and guided variants on rank 0 ----
     variants = None
@@ -277,6 +297,8 @@ def main():
         }
         if dslice is not None:
             res["dslice"] = dslice
+        if rowband is not None:
+            res["rowband"] = rowband
         if variants:
             res["variants"] = variants
         print(json.dumps(res), flush=True)

@@ -211,6 +211,28 @@ def test_slice_keys_min_equals_full(matcher, oracle, torch, cuts):
     assert np.array_equal(d.cpu().numpy(), disp)
 
 
+@pytest.mark.parametrize("G,agg,lr", [(2, "box", False), (8, "box", False), (3, "box", True), (4, "guided", False)])
+def test_rowband_bands_equal_full_frame(matcher, torch, G, agg, lr):
+    """The row-band partition's per-rank compute (sharding.band_disparity), run band by band on one
+    GPU, reassembles the single-pass map: bit-exact for box / LR, near-ties only for guided."""
+    from gpu_stereo_matching_amd import sharding
+    from oracle import oracle as O
+    L, R = O.synth_pair(555, 700, 203, 64)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    full = matcher.match_device(Lt, Rt, 5, 64, agg=agg, lr_check=lr)
+    parts = []
+    for k in range(G):
+        y0, y1 = sharding.band_rows(203, k, G)
+        if y1 > y0:
+            parts.append(sharding.band_disparity(matcher, Lt, Rt, 5, 64, y0, y1, agg, lr))
+    got = torch.cat(parts)
+    torch.cuda.synchronize()
+    if agg == "guided":
+        assert (got == full).float().mean().item() > 0.999
+    else:
+        assert torch.equal(got, full)
+
+
 def test_error_codes(sm, matcher):
     L = np.zeros((10, 10), np.uint8)
     with pytest.raises(sm.SMError) as e:
