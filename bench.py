@@ -132,16 +132,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    if distributed:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; SM_DIST_BACKEND=gloo with more ranks than GPUs is a rehearsal mode (ranks
+    # share devices, collectives go through the host) for boxes with fewer GPUs than ranks
+    backend = os.environ.get("SM_DIST_BACKEND", "nccl")
+    dev_index = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
+    if distributed:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import gpu_stereo_matching_amd as sm
 
     W, H, D, r, B = args.width, args.height, args.num_disp, args.radius, args.batch
-    m = sm.BlockMatcher(local_rank, W, H, 256)
+    m = sm.BlockMatcher(dev_index, W, H, 256)
 
     # synthetic frames for this rank: seeds seed + global frame index (disjoint per rank)
     Ls, Rs = [], []
@@ -223,7 +229,7 @@ def main():
         dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         dslice = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
-                  "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": "all_reduce MIN int32 (RCCL)",
+                  "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_reduce MIN int32 ({backend})",
                   "keys_bytes_per_frame": W * H * 4, "scaling": "strong"}
 
         # row bands of one frame (r-row halo, all-gather of uint8 bands)
@@ -242,7 +248,7 @@ def main():
         dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         rowband = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
-                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": "all_gather uint8 bands (RCCL)",
+                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_gather uint8 bands ({backend})",
                    "halo_rows": r, "scaling": "strong"}
 
     # ---- BASELINE configs, LR and guided variants on rank 0 ----

@@ -10,23 +10,10 @@ reports no match.
 import numpy as np
 import pytest
 
+from guided_check import tie_aware_check
+
 pytestmark = pytest.mark.gpu
-TOL = 2e-3
 EPS = 1e-4 * 255 * 255
-
-
-def tie_aware_check(gpu, q, best, D, W):
-    H = gpu.shape[0]
-    xs = np.arange(W)[None, :].repeat(H, 0)
-    ys = np.arange(H)[:, None].repeat(W, 1)
-    d_g = gpu.astype(np.int64)
-    q_g = q[np.clip(d_g, 0, D - 1), ys, xs]
-    ok_exact = d_g == best["disp"]
-    valid = d_g <= (W - xs)
-    near_tie = valid & (q_g <= best["best"] + TOL) & (q_g < 50.0 + TOL)
-    no_match = (d_g == 0) & (best["best"] >= 50.0 - TOL)
-    ok = ok_exact | near_tie | no_match
-    return ok, ok_exact
 
 
 @pytest.fixture(scope="module")

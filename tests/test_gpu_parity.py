@@ -228,7 +228,11 @@ def test_rowband_bands_equal_full_frame(matcher, torch, G, agg, lr):
     got = torch.cat(parts)
     torch.cuda.synchronize()
     if agg == "guided":
-        assert (got == full).float().mean().item() > 0.999
+        # band tiling changes the fp32 summation order: judged like the single pass, against fp64
+        from guided_check import tie_aware_check
+        disp_o, q, best = O.guided_disp(L, R, 5, 64, 1e-4 * 255 * 255, want_q=True)
+        ok, _ = tie_aware_check(got.cpu().numpy(), q, {"disp": disp_o, "best": best}, 64, L.shape[1])
+        assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
     else:
         assert torch.equal(got, full)
 
