@@ -80,16 +80,17 @@ def cpu_baseline(W, H, D, r, seed):
 # `batch` frames per call).  cfg1/cfg2 are quoted on the bundled Middlebury pairs; the bench uses
 # synthetic pairs of the same size because /root/reference is not on the GPU box.
 VARIANTS = (
-    # name, W, H, D, r, agg, lr, batch
-    ("cfg1 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, 16),
-    ("cfg2 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, 16),
-    ("cfg3 1080p 11x11 box+lr d128", 1920, 1080, 128, 5, "box", True, 4),
-    ("cfg3 1080p 11x11 guided d128", 1920, 1080, 128, 5, "guided", False, 4),
-    ("cfg3 1080p 11x11 guided+lr d128", 1920, 1080, 128, 5, "guided", True, 4),
-    ("cfg4 1080p 11x11 box d256", 1920, 1080, 256, 5, "box", False, 4),
-    ("cfg5 4K 11x11 box d192", 3840, 2160, 192, 5, "box", False, 2),
-    ("cfg5 4K 11x11 box+lr d192", 3840, 2160, 192, 5, "box", True, 2),
-    ("cfg5 4K 11x11 guided+lr d192", 3840, 2160, 192, 5, "guided", True, 2),
+    # name, W, H, D, r, agg, lr, median, batch
+    ("cfg1 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, False, 16),
+    ("cfg2 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, False, 16),
+    ("cfg3 1080p 11x11 box+lr d128", 1920, 1080, 128, 5, "box", True, False, 4),
+    ("cfg3 1080p 11x11 box+median7+lr d128", 1920, 1080, 128, 5, "box", True, True, 4),
+    ("cfg3 1080p 11x11 guided d128", 1920, 1080, 128, 5, "guided", False, False, 4),
+    ("cfg3 1080p 11x11 guided+lr d128", 1920, 1080, 128, 5, "guided", True, False, 4),
+    ("cfg4 1080p 11x11 box d256", 1920, 1080, 256, 5, "box", False, False, 4),
+    ("cfg5 4K 11x11 box d192", 3840, 2160, 192, 5, "box", False, False, 2),
+    ("cfg5 4K 11x11 box+lr d192", 3840, 2160, 192, 5, "box", True, False, 2),
+    ("cfg5 4K 11x11 guided+lr d192", 3840, 2160, 192, 5, "guided", True, False, 2),
 )
 
 
@@ -97,19 +98,19 @@ def run_variants(sm, torch, dev, stream, seed):
     out = {}
     m = sm.BlockMatcher(dev.index, 3840, 2160, 256)
     try:
-        for (name, W, H, D, r, agg, lr, B) in VARIANTS:
+        for (name, W, H, D, r, agg, lr, med, B) in VARIANTS:
             try:
                 pairs = [sm.synth_pair(seed + i, W, H, D) for i in range(B)]
                 Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
                 Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
                 o = torch.empty_like(Lt)
                 for _ in range(2):
-                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, stream=stream)
+                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, median=med, stream=stream)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 nrep = 10 if agg == "box" else 3
                 e0.record(stream)
                 for _ in range(nrep):
-                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, stream=stream)
+                    m.match_device(Lt, Rt, r, D, out_t=o, agg=agg, lr_check=lr, median=med, stream=stream)
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
                 ms = e0.elapsed_time(e1) / (nrep * B)

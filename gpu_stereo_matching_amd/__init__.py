@@ -22,13 +22,13 @@ from typing import Optional, Tuple
 import numpy as np
 
 from . import _capi
-from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK  # noqa: F401
+from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK, SM_MEDIAN  # noqa: F401
 from .synth import synth_pair  # noqa: F401
 from .gray import bgr_to_gray  # noqa: F401
 
 __all__ = [
     "BlockMatcher", "blockMatching_gpu", "block_matching_gpu", "SMError", "synth_pair", "bgr_to_gray",
-    "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "version",
+    "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "SM_MEDIAN", "version",
 ]
 
 DEFAULT_GUIDED_EPS = 1e-4 * 255.0 * 255.0
@@ -45,11 +45,11 @@ def _as_u8_image(a, name: str) -> np.ndarray:
     return a if a.flags.c_contiguous else np.ascontiguousarray(a)
 
 
-def _flags(agg: str, lr_check: bool) -> int:
+def _flags(agg: str, lr_check: bool, median: bool = False) -> int:
     if agg not in ("box", "guided"):
         raise ValueError("agg must be 'box' or 'guided'")
     f = SM_AGG_GUIDED if agg == "guided" else SM_AGG_BOX
-    return f | (SM_LR_CHECK if lr_check else 0)
+    return f | (SM_LR_CHECK if lr_check else 0) | (SM_MEDIAN if median else 0)
 
 
 class BlockMatcher:
@@ -85,7 +85,9 @@ class BlockMatcher:
         _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_GUIDED_EPS, float(eps)))
 
     # -- host-pointer path (blockMatching_gpu replacement) -------------------------------
-    def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False) -> np.ndarray:
+    def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
+              median: bool = False) -> np.ndarray:
+        """median=True: 7x7 median of the WTA map(s) (STMatching MeanFilter(disp, disp, 3)), before the LR check."""
         L = _as_u8_image(left, "left")
         R = _as_u8_image(right, "right")
         if L.shape != R.shape:
@@ -93,10 +95,10 @@ class BlockMatcher:
         H, W = L.shape
         out = np.empty((H, W), np.uint8)
         _capi.check(self._lib.sm_block_match_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
-                                                _flags(agg, lr_check), out.ctypes.data, W))
+                                                _flags(agg, lr_check, median), out.ctypes.data, W))
         return out
 
-    def match_lr(self, left, right, radius: int, num_disp: int, agg: str = "box"
+    def match_lr(self, left, right, radius: int, num_disp: int, agg: str = "box", median: bool = False
                  ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(checked disparity, right-view disparity, valid mask)."""
         L = _as_u8_image(left, "left")
@@ -106,7 +108,7 @@ class BlockMatcher:
         rd = np.empty((H, W), np.uint8)
         mask = np.empty((H, W), np.uint8)
         _capi.check(self._lib.sm_block_match_lr_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
-                                                   _flags(agg, True), out.ctypes.data, rd.ctypes.data,
+                                                   _flags(agg, True, median), out.ctypes.data, rd.ctypes.data,
                                                    mask.ctypes.data, W))
         return out, rd, mask
 
@@ -144,6 +146,16 @@ class BlockMatcher:
                                                  mapy_t.data_ptr(), W, out_t.data_ptr(), W, self._stream_ptr(stream)))
         return out_t
 
+    def median_device(self, src_t, radius: int = 3, out_t=None, stream=None):
+        """(2r+1)^2 median, replicate borders (ctmf, STMatching/ctmf.c), r in 1..3; src [H, W] uint8."""
+        import torch
+        H, W = src_t.shape
+        if out_t is None:
+            out_t = torch.empty_like(src_t)
+        _capi.check(self._lib.sm_median_u8_device(self._h, src_t.data_ptr(), W, H, W, radius, out_t.data_ptr(), W,
+                                                  self._stream_ptr(stream)))
+        return out_t
+
     def stage_ms(self) -> Tuple[float, float, float]:
         """(upload, match, download) ms of the last host call (Device.cu:218,238/257,292)."""
         u, m, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
@@ -159,7 +171,7 @@ class BlockMatcher:
         return ctypes.c_void_p(stream.cuda_stream)
 
     def match_device(self, left_t, right_t, radius: int, num_disp: int, out_t=None, agg: str = "box",
-                     lr_check: bool = False, stream=None):
+                     lr_check: bool = False, stream=None, median: bool = False):
         """left_t/right_t: uint8 cuda tensors [H, W] or [B, H, W] (contiguous). Async on `stream`."""
         import torch
         if left_t.dtype != torch.uint8 or right_t.dtype != torch.uint8:
@@ -173,7 +185,7 @@ class BlockMatcher:
         if out_t is None:
             out_t = torch.empty_like(left_t)
         _capi.check(self._lib.sm_match_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, B, H * W,
-                                              radius, num_disp, _flags(agg, lr_check), out_t.data_ptr(), W, H * W,
+                                              radius, num_disp, _flags(agg, lr_check, median), out_t.data_ptr(), W, H * W,
                                               self._stream_ptr(stream)))
         return out_t
 

@@ -28,11 +28,12 @@ __global__ __launch_bounds__(256) void mirror_kernel(const uint8_t* __restrict__
     dst[(int64_t)f * dstride + (int64_t)y * dpitch + x] = src[(int64_t)f * stride + (int64_t)y * pitch + (W - 1 - x)];
 }
 
-// StereoDisparity.cpp:136-147 with the right map stored mirrored (index W-1-u holds dR(u)):
+// StereoDisparity.cpp:136-147; the right map is stored plain or mirrored (index W-1-u holds dR(u)):
 //   d = dL(y,x); occ = x-d < 0 || d == 0 || |d - dR(y, x-d)| > 1;  out = occ ? 0 : d
-__global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* __restrict__ ld, int lpitch, int64_t lstride,
-                                                       const uint8_t* __restrict__ rdm, int rpitch, int64_t rstride,
-                                                       int W, uint8_t* __restrict__ out, int opitch, int64_t ostride,
+// `out` may alias `ld` (each thread reads its own pixel before writing it).
+__global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* ld, int lpitch, int64_t lstride,
+                                                       const uint8_t* __restrict__ rd, int rpitch, int64_t rstride,
+                                                       int mirrored, int W, uint8_t* out, int opitch, int64_t ostride,
                                                        uint8_t* __restrict__ right_out, uint8_t* __restrict__ mask_out,
                                                        int apitch, int64_t astride) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -40,17 +41,18 @@ __global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* __restrict
     const int f = blockIdx.z;
     if (x >= W) return;
     const uint8_t* lrow = ld + (int64_t)f * lstride + (int64_t)y * lpitch;
-    const uint8_t* rrow = rdm + (int64_t)f * rstride + (int64_t)y * rpitch;
+    const uint8_t* rrow = rd + (int64_t)f * rstride + (int64_t)y * rpitch;
     const int d = lrow[x];
     int occ = 1;
     if (x - d >= 0) {
-        const int dr = rrow[W - 1 - (x - d)];
+        const int u = x - d;
+        const int dr = rrow[mirrored ? W - 1 - u : u];
         const int diff = d - dr;
         occ = (d == 0) || diff > 1 || diff < -1;
     }
     out[(int64_t)f * ostride + (int64_t)y * opitch + x] = occ ? (uint8_t)0 : (uint8_t)d;
     if (mask_out) mask_out[(int64_t)f * astride + (int64_t)y * apitch + x] = (uint8_t)!occ;
-    if (right_out) right_out[(int64_t)f * astride + (int64_t)y * apitch + x] = rrow[W - 1 - x];
+    if (right_out) right_out[(int64_t)f * astride + (int64_t)y * apitch + x] = rrow[mirrored ? W - 1 - x : x];
 }
 
 }  // namespace
@@ -69,13 +71,13 @@ hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t st
     return hipGetLastError();
 }
 
-hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride, const uint8_t* right_disp_mirrored,
-                           int rpitch, int64_t rstride, int W, int H, int batch, uint8_t* out, int opitch,
-                           int64_t ostride, uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
-                           hipStream_t s) {
+hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride, const uint8_t* right_disp,
+                           int rpitch, int64_t rstride, int right_mirrored, int W, int H, int batch, uint8_t* out,
+                           int opitch, int64_t ostride, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
+                           int64_t aux_stride, hipStream_t s) {
     dim3 grid((W + 255) / 256, H, batch);
-    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, s, left_disp, lpitch, lstride, right_disp_mirrored,
-                       rpitch, rstride, W, out, opitch, ostride, right_out, mask_out, aux_pitch, aux_stride);
+    hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, s, left_disp, lpitch, lstride, right_disp, rpitch, rstride,
+                       right_mirrored, W, out, opitch, ostride, right_out, mask_out, aux_pitch, aux_stride);
     return hipGetLastError();
 }
 

@@ -372,13 +372,13 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     }
 }
 
-// Right view + LR check for one image row per block.  Right key of u = min over the tiles whose
+// Right view (+ LR check when `check`) for one image row per block.  Right key of u = min over the tiles whose
 // partial rows cover u (x0 - DMAX - 1 <= u < x0 + TW, x0 <= u + d_hi - 1); dR = key & 0xFF with no
 // threshold (StereoHelper.cpp:131-154).  Then StereoDisparity.cpp:136-147 on the row:
 //   d = dL(x); occ = x-d < 0 || d == 0 || |d - dR(x-d)| > 1;  out = occ ? 0 : d.
 __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
                                                               int tiles_y, int TW, int PW, int dmax, int d_hi, int W,
-                                                              int H, uint8_t* disp, int opitch, int64_t ostride,
+                                                              int H, int check, uint8_t* disp, int opitch, int64_t ostride,
                                                               uint8_t* __restrict__ right_out,
                                                               uint8_t* __restrict__ mask_out, int apitch,
                                                               int64_t astride) {
@@ -397,6 +397,7 @@ __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __
         dr_row[u] = dr;
         if (rrow) rrow[u] = dr;
     }
+    if (!check) return;
     __syncthreads();
     uint8_t* drow = disp + (int64_t)f * ostride + (int64_t)y * opitch;
     uint8_t* mrow = mask_out ? mask_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
@@ -414,7 +415,8 @@ __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __
 
 // Output buffers of the fused right view (launch_box_match_lr).
 struct RightOut {
-    uint8_t* right;   // optional dR
+    int check;        // 1: apply the LR check to a.disp; 0: only produce dR
+    uint8_t* right;   // dR (optional when check)
     uint8_t* mask;    // optional valid mask
     int pitch;
     int64_t stride;
@@ -433,8 +435,8 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(right_reduce_lr_kernel, dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart, tiles_x,
-                           tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, a.disp, a.out_pitch, a.out_frame_stride,
-                           ro->right, ro->mask, ro->pitch, ro->stride);
+                           tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
+                           a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
     } else {
         hipLaunchKernelGGL((box_match_kernel<R, DMAX, false>), dim3((unsigned)blocks), dim3(64 * kWaves<false, R>),
                            (size_t)G::LDS_BYTES, s, a, tiles_x, tiles_y);
@@ -529,10 +531,10 @@ size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch) {
     }
 }
 
-hipError_t launch_box_match_lr(const MatchArgs& a, int batch, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
-                               int64_t aux_stride, hipStream_t s) {
-    if (a.d_lo != 0 || a.valid_mode != 0 || !a.disp || !a.rpart) return hipErrorInvalidValue;
-    const RightOut ro{right_out, mask_out, aux_pitch, aux_stride};
+hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,
+                               int aux_pitch, int64_t aux_stride, hipStream_t s) {
+    if (a.d_lo != 0 || a.valid_mode != 0 || !a.disp || !a.rpart || (!check && !right_out)) return hipErrorInvalidValue;
+    const RightOut ro{check, right_out, mask_out, aux_pitch, aux_stride};
     switch (a.radius) {
         case 0: return launch_r<0, true>(a, batch, &ro, s);
         case 1: return launch_r<1, true>(a, batch, &ro, s);

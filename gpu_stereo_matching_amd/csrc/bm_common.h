@@ -29,20 +29,25 @@ constexpr int kMaxFastRadius = 7;  // u16 packed sums stay < 2^16 up to r = 7 (1
 // Host-side launchers (bm_box.hip, bm_aux.hip).
 hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s);
 hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s);
-// Box matching + right view + LR check in two launches (radius <= kMaxFastRadius, d_lo == 0):
-// a.disp receives the checked left disparity, right_out/mask_out (optional) dR and the valid mask.
-hipError_t launch_box_match_lr(const MatchArgs& a, int batch, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
-                               int64_t aux_stride, hipStream_t s);
+// Box matching + right view (+ LR check) in two launches (radius <= kMaxFastRadius, d_lo == 0).
+// check = 1: a.disp receives the checked left disparity, right_out/mask_out (optional) dR and the
+// valid mask.  check = 0: a.disp the unchecked left map and right_out (required) dR.
+hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,
+                               int aux_pitch, int64_t aux_stride, hipStream_t s);
 size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch);
 hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key,
                                uint8_t* disp, int out_pitch, hipStream_t s);
 hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch,
                          uint8_t* dst, int dst_pitch, int64_t dst_stride, hipStream_t s);
+// right_mirrored: 1 if the right map is stored mirrored (index W-1-u holds dR(u)), 0 if plain
 hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride,
-                           const uint8_t* right_disp_mirrored, int rpitch, int64_t rstride,
+                           const uint8_t* right_disp, int rpitch, int64_t rstride, int right_mirrored,
                            int W, int H, int batch, uint8_t* out, int opitch, int64_t ostride,
                            uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
                            hipStream_t s);
+// (2r+1)^2 median with replicate borders, radius 1..3 (bm_post.hip)
+hipError_t launch_median(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch, int radius,
+                         uint8_t* dst, int dpitch, int64_t dstride, hipStream_t s);
 
 hipError_t launch_bgr_to_gray(const uint8_t* src, int W, int H, int pitch, int channels, uint8_t* dst, int dpitch,
                               hipStream_t s);

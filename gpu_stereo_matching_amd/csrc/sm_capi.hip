@@ -28,6 +28,9 @@ struct sm_handle {
     // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
     uint8_t* d_lr = nullptr;
     size_t lr_bytes = 0;
+    // right-map / mask staging of the host LR entry point (grown on demand)
+    uint8_t* d_aux = nullptr;
+    size_t aux_bytes = 0;
     // fused right view: per-tile right-key partials (grown on demand)
     uint32_t* d_rpart = nullptr;
     size_t rpart_bytes = 0;
@@ -97,35 +100,43 @@ int ensure_rpart(sm_handle* h, size_t bytes) {
     return SM_OK;
 }
 
-// Core device-side pass over `batch` frames.
+// Core device-side pass over `batch` frames.  Workspace planes (d_lr) are dense W x H frames.
+//   left map  : matched straight into `disp`, or into a workspace plane when SM_MEDIAN filters it
+//               into `disp` afterwards (StereoDisparity.cpp:85/119);
+//   right map : fused with the left pass for box r <= 7, else matched on the mirrored
+//               pair (valid d <= x, no threshold) and kept mirrored;
+//   LR check  : StereoDisparity.cpp:136-147 on the (median-filtered, :119-126) maps.
 int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
                uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
     const bool lr = (flags & SM_LR_CHECK) != 0 || right_out || mask_out;
-    if (guided) {
-        if (lr) {
-            // guided + LR: right view by mirroring, same as the box path below
-            const int64_t P = (int64_t)W * H;
-            int rc = ensure_lr(h, (size_t)(3 * P * batch));
-            if (rc) return rc;
-            uint8_t* mL = h->d_lr;
-            uint8_t* mR = mL + P * batch;
-            uint8_t* rdm = mR + P * batch;
-            SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0,
-                                          disp, opitch, ostride, s));
-            SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
-            SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
-            SM_HIP(sm::launch_guided_match(mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, rdm, W,
-                                          P, s));
-            SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rdm, W, P, W, H, batch, disp, opitch, ostride,
-                                       right_out, mask_out, apitch, astride, s));
-            return SM_OK;
-        }
-        SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, disp,
-                                      opitch, ostride, s));
-        return SM_OK;
+    const bool med = (flags & SM_MEDIAN) != 0;
+    constexpr int kMedianRadius = 3;   // MeanFilter(disp, disp, 3)
+    const int64_t P = (int64_t)W * H;
+    const int64_t PB = P * batch;
+    const bool fused_right = lr && !guided && radius <= sm::kMaxFastRadius;
+
+    // workspace: [left raw (med)] [right (lr)] [right filtered (lr && med)] [mirrored L, R (lr, not fused)]
+    const int64_t n_planes = (med ? 1 : 0) + (lr ? 1 : 0) + (lr && med ? 1 : 0) + (lr && !fused_right ? 2 : 0);
+    if (n_planes > 0) {
+        int rc = ensure_lr(h, (size_t)(n_planes * PB));
+        if (rc) return rc;
     }
+    uint8_t* ws = h->d_lr;
+    uint8_t* left_raw = med ? ws : nullptr;
+    if (med) ws += PB;
+    uint8_t* right_map = lr ? ws : nullptr;   // plain (fused) or mirrored
+    if (lr) ws += PB;
+    uint8_t* right_med = (lr && med) ? ws : nullptr;
+    if (lr && med) ws += PB;
+    uint8_t* mL = (lr && !fused_right) ? ws : nullptr;
+    uint8_t* mR = mL ? mL + PB : nullptr;
+
+    // ---- left map ----
+    uint8_t* lmap = med ? left_raw : disp;
+    const int lpitch = med ? W : opitch;
+    const int64_t lstride = med ? P : ostride;
     sm::MatchArgs a{};
     a.left = L;
     a.right = R;
@@ -139,49 +150,58 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     a.valid_mode = 0;
     a.seed_key = seed_key(radius);
     a.thresh_key = seed_key(radius);
-    a.disp = disp;
-    a.out_pitch = opitch;
-    a.out_frame_stride = ostride;
+    a.disp = lmap;
+    a.out_pitch = lpitch;
+    a.out_frame_stride = lstride;
     a.keys = nullptr;
     a.rpart = nullptr;
-    if (!lr) {
-        SM_HIP(sm::launch_box_match(a, batch, s));
-        return SM_OK;
-    }
-    if (radius <= sm::kMaxFastRadius) {
-        // right view fused into the matching pass (C_R(u,d) = C_L(u+d,d), StereoHelper.cpp:156-180)
+    if (fused_right) {
         int rc = ensure_rpart(h, sm::box_right_partial_bytes(W, H, radius, D, batch));
         if (rc) return rc;
         a.rpart = h->d_rpart;
-        SM_HIP(sm::launch_box_match_lr(a, batch, right_out, mask_out, apitch, astride, s));
-        return SM_OK;
+        if (!med) {   // match + right view + check in one pass over the partials
+            SM_HIP(sm::launch_box_match_lr(a, batch, 1, right_out, mask_out, apitch, astride, s));
+            return SM_OK;
+        }
+        SM_HIP(sm::launch_box_match_lr(a, batch, 0, right_map, nullptr, W, P, s));
+    } else if (guided) {
+        SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
+                                      lstride, s));
+    } else {
+        SM_HIP(sm::launch_box_match(a, batch, s));
     }
-    SM_HIP(sm::launch_box_match(a, batch, s));
+    if (med) SM_HIP(sm::launch_median(left_raw, W, H, W, P, batch, kMedianRadius, disp, opitch, ostride, s));
+    if (!lr) return SM_OK;
 
-    // Right view (StereoHelper.cpp:156-180 + :131-154) as the left matcher on the mirrored pair,
-    // validity d <= x (mirrored) and no threshold; then the StereoDisparity.cpp:136-147 check.
-    const int64_t P = (int64_t)W * H;
-    int rc = ensure_lr(h, (size_t)(3 * P * batch));
-    if (rc) return rc;
-    uint8_t* mL = h->d_lr;
-    uint8_t* mR = mL + P * batch;
-    uint8_t* rdm = mR + P * batch;
-    SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
-    SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
-    sm::MatchArgs b = a;
-    b.left = mL;
-    b.right = mR;
-    b.pitch = W;
-    b.frame_stride = P;
-    b.valid_mode = 1;
-    b.seed_key = 0xFFFFFFFFu;
-    b.thresh_key = 0xFFFFFFFFu;
-    b.disp = rdm;
-    b.out_pitch = W;
-    b.out_frame_stride = P;
-    SM_HIP(sm::launch_box_match(b, batch, s));
-    SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rdm, W, P, W, H, batch, disp, opitch, ostride, right_out,
-                               mask_out, apitch, astride, s));
+    // ---- right map on the mirrored pair (StereoHelper.cpp:156-180 + :131-154) ----
+    if (!fused_right) {
+        SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
+        SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
+        if (guided) {
+            SM_HIP(sm::launch_guided_match(mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, right_map, W, P,
+                                          s));
+        } else {
+            sm::MatchArgs b = a;
+            b.left = mL;
+            b.right = mR;
+            b.pitch = W;
+            b.frame_stride = P;
+            b.valid_mode = 1;
+            b.seed_key = 0xFFFFFFFFu;
+            b.thresh_key = 0xFFFFFFFFu;
+            b.disp = right_map;
+            b.out_pitch = W;
+            b.out_frame_stride = P;
+            SM_HIP(sm::launch_box_match(b, batch, s));
+        }
+    }
+    const uint8_t* rcheck = right_map;
+    if (med) {   // the median commutes with the mirror, so a mirrored map is filtered as is
+        SM_HIP(sm::launch_median(right_map, W, H, W, P, batch, kMedianRadius, right_med, W, P, s));
+        rcheck = right_med;
+    }
+    SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rcheck, W, P, fused_right ? 0 : 1, W, H, batch, disp, opitch,
+                               ostride, right_out, mask_out, apitch, astride, s));
     return SM_OK;
 }
 
@@ -200,14 +220,19 @@ int host_match(sm_handle* h, const uint8_t* left, const uint8_t* right, int widt
     const int64_t P = (int64_t)width * height;
     uint8_t* aux = nullptr;
     if (right_out || mask_out) {
-        rc = ensure_lr(h, (size_t)(5 * P));  // 3P for the LR pass + 2P for right/mask outputs
-        if (rc) return rc;
+        if (h->aux_bytes < (size_t)(2 * P)) {
+            if (h->d_aux) (void)hipFree(h->d_aux);
+            h->d_aux = nullptr;
+            h->aux_bytes = 0;
+            SM_HIP(hipMalloc(&h->d_aux, (size_t)(2 * P)));
+            h->aux_bytes = (size_t)(2 * P);
+        }
+        aux = h->d_aux;
     }
     SM_HIP(hipEventRecord(h->ev[0], s));
     SM_HIP(hipMemcpy2DAsync(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(hipMemcpy2DAsync(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(hipEventRecord(h->ev[1], s));
-    if (right_out || mask_out) aux = h->d_lr + 3 * P;
     rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
                     right_out ? aux : nullptr, mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
@@ -283,6 +308,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_disp);
     (void)hipFree(h->d_lr);
     (void)hipFree(h->d_rpart);
+    (void)hipFree(h->d_aux);
     (void)hipFree(h->d_bgr);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -398,6 +424,18 @@ SM_API int sm_remap_u8_device(sm_handle* h, const uint8_t* d_src, int width, int
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(sm::launch_remap(d_src, width, height, pitch, d_mapx, d_mapy, map_pitch, d_dst, dst_pitch,
                             (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_median_u8_device(sm_handle* h, const uint8_t* d_src, int width, int height, int pitch, int radius,
+                               uint8_t* d_dst, int dst_pitch, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_src || !d_dst || width <= 0 || height <= 0 || pitch < width || dst_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad median arguments");
+    if (radius < 1 || radius > 3) return fail(SM_ERR_INVALID_ARG, "median radius %d out of [1,3]", radius);
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_median(d_src, width, height, pitch, (int64_t)pitch * height, 1, radius, d_dst, dst_pitch,
+                             (int64_t)dst_pitch * height, (hipStream_t)stream));
     return SM_OK;
 }
 

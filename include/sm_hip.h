@@ -44,8 +44,12 @@ enum {
 enum {
     SM_AGG_BOX = 0u,        /* (2r+1)^2 zero-padded SAD window: the reference's kernalFindCorr */
     SM_AGG_GUIDED = 1u,     /* guided-filter aggregation of the AD volume (this build's extension) */
-    SM_LR_CHECK = 2u        /* left-right consistency (STMatching/StereoDisparity.cpp:136-147):
+    SM_LR_CHECK = 2u,       /* left-right consistency (STMatching/StereoDisparity.cpp:136-147):
                                occluded pixels are written as 0 */
+    SM_MEDIAN = 4u          /* 7x7 median post-filter of the WTA map(s), STMatching's
+                               MeanFilter(disp, disp, 3) = ctmf (Toolkit.cpp:33-48); with
+                               SM_LR_CHECK both maps are filtered before the check, in the
+                               order of StereoDisparity.cpp:119-126 */
 };
 
 /* ---- scalar parameters (sm_set_param_f) ---- */
@@ -70,7 +74,7 @@ SM_API int sm_set_param_f(sm_handle *h, int param, float value);
 /* Host-pointer entry point — the blockMatching_gpu replacement.
  * left/right: uint8 gray, `height` rows of `width` bytes at row stride `pitch` (>= width).
  * disp_out: uint8, `height` rows at stride `out_pitch`.  Synchronous, like the reference.
- * flags: SM_AGG_BOX | SM_AGG_GUIDED, optionally | SM_LR_CHECK. */
+ * flags: SM_AGG_BOX | SM_AGG_GUIDED, optionally | SM_LR_CHECK | SM_MEDIAN. */
 SM_API int sm_block_match_u8(sm_handle *h, const uint8_t *left, const uint8_t *right,
                              int width, int height, int pitch, int radius, int num_disp,
                              unsigned flags, uint8_t *disp_out, int out_pitch);
@@ -123,6 +127,12 @@ SM_API int sm_bgr_to_gray_device(sm_handle *h, const uint8_t *d_bgr, int width, 
 SM_API int sm_remap_u8_device(sm_handle *h, const uint8_t *d_src, int width, int height, int pitch,
                               const float *d_mapx, const float *d_mapy, int map_pitch,
                               uint8_t *d_dst, int dst_pitch, void *stream);
+
+/* ---- post-filter ----
+ * (2r+1)^2 median with replicate borders, r in 1..3: ctmf (STMatching/ctmf.c:378-433) as called
+ * by MeanFilter (Toolkit.cpp:33-48).  Not in place: d_src and d_dst must not overlap. */
+SM_API int sm_median_u8_device(sm_handle *h, const uint8_t *d_src, int width, int height, int pitch,
+                               int radius, uint8_t *d_dst, int dst_pitch, void *stream);
 
 /* imread -> cvtColor -> blockMatching_gpu in one call (Caller.cpp:12-19): BGR(A) host frames
  * are uploaded, converted to gray on the GPU and matched.  Synchronous. */

@@ -482,3 +482,42 @@ ORA_API void ora_synth_pair(uint64_t seed, int W, int H, int D, uint8_t *L, uint
         }
     }
 }
+
+/* ------------------------------------------------------------------------- */
+/* §8f rank 4: the disparity median post-filter of the reference's STMatching */
+/* pipeline, MeanFilter(disp, disp, 3) (Toolkit.cpp:33-48, used at            */
+/* StereoDisparity.cpp:85,119,126,156) = ctmf() (STMatching/ctmf.c:378-433,    */
+/* Perreault & Hebert's constant-time median).  Restated from its source:      */
+/* the column histograms are seeded with row 0 r+1 times and re-read row      */
+/* MIN(m-1, i+r) (ctmf.c:230-257), the row histograms do the same with columns */
+/* (:263-315), so the window is replicate-padded; the output is the first      */
+/* value whose cumulative count exceeds t = 2r^2 + 2r (:284, :322-329), i.e.   */
+/* the (t+1)-th smallest of the (2r+1)^2 values.  The stripe split (:421-431)  */
+/* overlaps stripes by 2r and does not change the result.  Parity unpinned:    */
+/* the reference ships no median vectors and building ctmf.c here was refused. */
+/* ------------------------------------------------------------------------- */
+ORA_API void ora_median_u8(const uint8_t *src, int W, int H, int r, uint8_t *dst)
+{
+    const int t = 2 * r * r + 2 * r;
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            int hist[256];
+            memset(hist, 0, sizeof(hist));
+            for (int i = -r; i <= r; ++i) {
+                int yy = y + i;
+                yy = yy < 0 ? 0 : (yy > H - 1 ? H - 1 : yy);
+                for (int j = -r; j <= r; ++j) {
+                    int xx = x + j;
+                    xx = xx < 0 ? 0 : (xx > W - 1 ? W - 1 : xx);
+                    hist[src[(int64_t)yy * W + xx]]++;
+                }
+            }
+            int sum = 0, v = 0;
+            for (; v < 256; ++v) {
+                sum += hist[v];
+                if (sum > t) break;
+            }
+            dst[(int64_t)y * W + x] = (uint8_t)v;
+        }
+    }
+}

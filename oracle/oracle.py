@@ -57,6 +57,7 @@ def lib():
         L.ora_box_mean_f64.argtypes = [_f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p]
         L.ora_remap.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                 ctypes.POINTER(ctypes.c_float), _u8p]
+        L.ora_median_u8.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p]
         L.ora_synth_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
         _lib = L
     return _lib
@@ -183,6 +184,15 @@ def remap(src, mapx, mapy):
     out = np.empty((H, W), np.uint8)
     fp = ctypes.POINTER(ctypes.c_float)
     lib().ora_remap(_p(src, _u8p), W, H, mapx.ctypes.data_as(fp), mapy.ctypes.data_as(fp), _p(out, _u8p))
+    return out
+
+
+def median(src, r: int):
+    """ctmf (STMatching/ctmf.c) restatement: (2r+1)^2 median, replicate borders."""
+    src = _img(src)
+    H, W = src.shape
+    out = np.empty((H, W), np.uint8)
+    lib().ora_median_u8(_p(src, _u8p), W, H, r, _p(out, _u8p))
     return out
 
 

@@ -130,3 +130,16 @@ def test_guided_large_eps_tends_to_box_mean(oracle):
         oracle.lib().ora_box_mean_f64(ad.ctypes.data_as(oracle._f64p), 24, 20, 2, m1.ctypes.data_as(oracle._f64p))
         oracle.lib().ora_box_mean_f64(m1.ctypes.data_as(oracle._f64p), 24, 20, 2, m2.ctypes.data_as(oracle._f64p))
         np.testing.assert_allclose(q[d], m2, atol=1e-6)
+
+
+@pytest.mark.parametrize("r", [1, 2, 3])
+@pytest.mark.parametrize("W,H", [(1, 1), (2, 9), (7, 7), (37, 53)])
+def test_median_restatement_matches_numpy(oracle, r, W, H):
+    """ora_median_u8 (ctmf restatement) == an independent numpy edge-padded window median."""
+    from numpy.lib.stride_tricks import sliding_window_view
+    a = np.random.default_rng(W + 10 * H + r).integers(0, 256, (H, W), dtype=np.uint8)
+    p = np.pad(a, r, mode="edge")
+    k = 2 * r + 1
+    w = sliding_window_view(p, (k, k)).reshape(H, W, k * k)
+    want = np.sort(w, axis=2)[:, :, (k * k) // 2]
+    assert np.array_equal(oracle.median(a, r), want)

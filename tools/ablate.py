@@ -6,7 +6,8 @@ import gpu_stereo_matching_amd._capi as C
 C.load(sys.argv[1])
 import gpu_stereo_matching_amd as sm
 m = sm.BlockMatcher(0, 1920, 1080, 256)
-pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(4)]
+NB = int(os.environ.get('SM_AB_B', '4'))
+pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(NB)]
 Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda(); Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
 out = torch.empty_like(Lt)
 LR = bool(int(os.environ.get('SM_AB_LR', '0')))
@@ -20,4 +21,4 @@ e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=Tr
 e0.record()
 for _ in range(NIT): m.match_device(Lt, Rt, RAD, DD, out_t=out, lr_check=LR, agg=AGG)
 e1.record(); torch.cuda.synchronize()
-print(sys.argv[1], "ms/frame", e0.elapsed_time(e1) / NIT / 4)
+print(sys.argv[1], "ms/frame", e0.elapsed_time(e1) / NIT / NB)
