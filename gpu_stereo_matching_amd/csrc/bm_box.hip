@@ -135,8 +135,9 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     const int lane = tid & 63;
 
     const int tiles = tiles_x * tiles_y;
-    const int frame = blockIdx.x / tiles;
-    const int t = blockIdx.x - frame * tiles;
+    const int tile_id = xcd_tile(blockIdx.x, gridDim.x);   // [frame][ty][tx]
+    const int frame = tile_id / tiles;
+    const int t = tile_id - frame * tiles;
     const int ty = t / tiles_x;
     const int tx = t - ty * tiles_x;
     const int x0 = tx * G::TW;
@@ -364,7 +365,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     }
     if constexpr (RIGHT) {
         // rb is untouched by the fold (which aliases the CS area); rows past H are never read
-        uint32_t* P = a.rpart + (int64_t)blockIdx.x * (kTileH * G::PW);   // [frame][ty][tx][kTileH][PW]
+        uint32_t* P = a.rpart + (int64_t)tile_id * (kTileH * G::PW);   // [frame][ty][tx][kTileH][PW]
         for (int e = tid; e < kTileH * G::PW; e += kThreads) {
             const int j = e / G::PW;
             P[e] = rb[j * G::RBW + (e - j * G::PW)];

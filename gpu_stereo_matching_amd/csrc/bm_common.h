@@ -24,6 +24,16 @@ struct MatchArgs {
 };
 
 constexpr int kMaxDisp = 256;      // uint8 output / 8-bit d field of the packed key
+constexpr int kNumXcd = 8;         // MI355X: 8 XCDs, each with its own L2
+
+// Workgroups are dispatched round-robin over the XCDs (blockIdx % 8).  Remapping so that XCD k
+// works through a contiguous run of tile indices keeps neighbouring tiles, whose right bands
+// overlap by (D + 64 - TW) / (D + 64), in one L2.
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+    const int per = nb / kNumXcd, rem = nb - per * kNumXcd;
+    const int x = b % kNumXcd, i = b / kNumXcd;
+    return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
 constexpr int kMaxFastRadius = 7;  // u16 packed sums stay < 2^16 up to r = 7 (15*15*255 = 57375)
 
 // Host-side launchers (bm_box.hip, bm_aux.hip).

@@ -100,8 +100,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     uint8_t* rb = smem + G::CS_BYTES + G::MM_BYTES + G::AB_BYTES;                      // [PH][RBW]
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int frame = blockIdx.x / tiles;
-    const int t = blockIdx.x - frame * tiles;
+    const int tile_id = xcd_tile(blockIdx.x, gridDim.x);
+    const int frame = tile_id / tiles;
+    const int t = tile_id - frame * tiles;
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
     const int x0 = tx * G::TW, y0 = ty * G::TH;
     const int px0 = x0 - 2 * R, py0 = y0 - 2 * R;      // P region origin (image coords)
