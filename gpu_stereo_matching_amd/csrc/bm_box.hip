@@ -152,32 +152,50 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     const int base = (x0 - R - d_lo - dspan) & ~3;   // image column of rs[.][0] (floor to x4)
     const int off0 = x0 - R - base;                  // rs index of (column c = x0-R+lane) at d = 0, minus lane
 
-    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8, from dword loads
-    //      (all issued before any LDS write; image borders read as 0) ----
-#if SM_ABLATE & 8
-    if (false)
-#endif
-    {
-        constexpr int N = G::ROWS * G::NDW;
+    // ---- stage the right band: rs[i][k] = R(y, base+k) | R(y, base+k-1) << 8, from dword loads,
+    //      and the left tile (64 columns from x0-R) into the CS area.  Interior tiles (every row
+    //      and column of both bands inside the image: the common case) take a branch-free path so
+    //      all loads issue before the first wait; border tiles read outside bytes as 0 ----
+    const int c = x0 - R + lane;                   // image column of CS column `lane`
+    const int lbase = (x0 - R) & ~3;
+    uint8_t* ls = smem;                            // [ROWS][LSTR] bytes, aliases cs (unused yet)
+    constexpr int NR = G::ROWS * G::NDW;
+    constexpr int NL = G::ROWS * (G::LSTR / 4);
+    const bool interior = (y0 - R >= 0) && (y0 + kTileH + R <= H) && (base - 4 >= 0) &&
+                          (base + 4 * G::NDW <= W) && (lbase >= 0) && (lbase + G::LSTR <= W);
+    if (interior) {
+        const uint8_t* r0 = Rf + (int64_t)(y0 - R) * a.pitch + base;
+        const uint8_t* l0 = Lf + (int64_t)(y0 - R) * a.pitch + lbase;
 #pragma unroll 4
-        for (int e = tid; e < N; e += kThreads) {
+        for (int e = tid; e < NR; e += kThreads) {
             const int i = e / G::NDW, j = e - (e / G::NDW) * G::NDW;
-            const int y = y0 - R + i, col = base + 4 * j;
-            const uint32_t cur = ld_u32(Rf, y, col, W, H, a.pitch);
-            const uint32_t prv = ld_u32(Rf, y, col - 4, W, H, a.pitch);
+            const uint8_t* p = r0 + (int64_t)i * a.pitch + 4 * j;
+            uint32_t cur, prv;
+            __builtin_memcpy(&cur, p, 4);
+            __builtin_memcpy(&prv, p - 4, 4);
             uint2 v;
             v.x = __builtin_amdgcn_perm(cur, prv, 0x04050304u);   // [b0, p3, b1, b0]
             v.y = __builtin_amdgcn_perm(cur, cur, 0x06070506u);   // [b2, b1, b3, b2]
             *reinterpret_cast<uint2*>(rs + i * G::RW + 4 * j) = v;
         }
-    }
-    // ---- stage the left tile (64 columns from x0-R) into the CS area, then pack this lane's
-    //      column 4 rows per dword ----
-    const int c = x0 - R + lane;                   // image column of CS column `lane`
-    const int lbase = (x0 - R) & ~3;
-    {
-        uint8_t* ls = smem;                        // [ROWS][LSTR] bytes, aliases cs (unused yet)
-        constexpr int NL = G::ROWS * (G::LSTR / 4);
+#pragma unroll 4
+        for (int e = tid; e < NL; e += kThreads) {
+            const int i = e / (G::LSTR / 4), j = e - (e / (G::LSTR / 4)) * (G::LSTR / 4);
+            uint32_t v;
+            __builtin_memcpy(&v, l0 + (int64_t)i * a.pitch + 4 * j, 4);
+            *reinterpret_cast<uint32_t*>(ls + i * G::LSTR + 4 * j) = v;
+        }
+    } else {
+        for (int e = tid; e < NR; e += kThreads) {
+            const int i = e / G::NDW, j = e - (e / G::NDW) * G::NDW;
+            const int y = y0 - R + i, col = base + 4 * j;
+            const uint32_t cur = ld_u32(Rf, y, col, W, H, a.pitch);
+            const uint32_t prv = ld_u32(Rf, y, col - 4, W, H, a.pitch);
+            uint2 v;
+            v.x = __builtin_amdgcn_perm(cur, prv, 0x04050304u);
+            v.y = __builtin_amdgcn_perm(cur, cur, 0x06070506u);
+            *reinterpret_cast<uint2*>(rs + i * G::RW + 4 * j) = v;
+        }
         for (int e = tid; e < NL; e += kThreads) {
             const int i = e / (G::LSTR / 4), j = e - (e / (G::LSTR / 4)) * (G::LSTR / 4);
             *reinterpret_cast<uint32_t*>(ls + i * G::LSTR + 4 * j) = ld_u32(Lf, y0 - R + i, lbase + 4 * j, W, H, a.pitch);
