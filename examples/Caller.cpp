@@ -1,4 +1,4 @@
-// Caller.cpp — singleFrame() as in BlockMatching/Caller.cpp:9-25, on the MI355X engine.
+// Caller.cpp — the reference's demos (BlockMatching/Caller.cpp) on the MI355X engine.
 // Without OpenCV in this image, images are 8-bit PGM (gray already: the reference converts with
 // cvtColor(CV_BGR2GRAY) at Caller.cpp:15-16; tests/golden holds the converted pairs) and the
 // disparity is written as PGM instead of imshow.
@@ -8,6 +8,8 @@
 #include <fstream>
 #include <iostream>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "Caller.h"
 #include "stereo_bm.hpp"
@@ -54,5 +56,55 @@ void singleFrame() {
     write_pgm(env_or("SM_OUT", "disp.pgm"), disp);                    // imshow("disp", disp) in the reference
 }
 
-void remapTest() { std::cout << "remapTest: rectification is outside this engine's scope" << std::endl; }
-void cvtColorTest() { std::cout << "cvtColorTest: gray conversion is outside this engine's scope" << std::endl; }
+// remapTest (Caller.cpp:27-74): rectify a pair with remap_gpu.  Without OpenCV/YAML in this
+// image the CV_32FC1 maps come from raw float files (SM_MAPX / SM_MAPY, rows*cols floats each)
+// instead of LoadDataBatch + Rectify; the left result is written as PGM instead of imshow.
+static bool read_f32(const std::string& path, sm::Mat& m, int rows, int cols) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    m.create(rows, cols, CV_32FC1);
+    f.read(reinterpret_cast<char*>(m.data), (std::streamsize)(m.step * rows));
+    return (bool)f;
+}
+
+void remapTest() {
+    sm::Mat left, right, mapX1, mapY1;
+    if (!read_pgm(env_or("SM_LEFT", "view1_.pgm"), left) || !read_pgm(env_or("SM_RIGHT", "view5_.pgm"), right)) {
+        std::cerr << "cannot read the pair" << std::endl;
+        std::exit(2);
+    }
+    const int rows = left.rows, cols = left.cols, total = rows * cols;
+    if (!read_f32(env_or("SM_MAPX", "mapx.f32"), mapX1, rows, cols) ||
+        !read_f32(env_or("SM_MAPY", "mapy.f32"), mapY1, rows, cols)) {
+        std::cerr << "cannot read the maps" << std::endl;
+        std::exit(2);
+    }
+    sm::Mat result(rows, cols);
+    auto t0 = std::chrono::steady_clock::now();
+    remap_gpu(left, right, mapX1, mapY1, mapX1, mapY1, rows, cols, total, result.data);
+    auto t1 = std::chrono::steady_clock::now();
+    std::cout << "GPU Remap : " << std::chrono::duration<double, std::milli>(t1 - t0).count() << std::endl;
+    write_pgm(env_or("SM_OUT", "remap.pgm"), result);
+}
+
+// cvtColorTest (Caller.cpp:76-113): BGR -> gray with cvtColor_gpu on a binary PPM (P6, RGB order on
+// disk, swapped to BGR in memory like imread), written as PGM.
+void cvtColorTest() {
+    std::ifstream f(env_or("SM_BGR", "view1_.ppm"), std::ios::binary);
+    std::string magic;
+    int w = 0, h = 0, maxv = 0;
+    if (!(f >> magic >> w >> h >> maxv) || magic != "P6" || maxv != 255) {
+        std::cerr << "cannot read PPM" << std::endl;
+        std::exit(2);
+    }
+    f.get();
+    std::vector<uchar3> bgr((size_t)w * h);
+    f.read(reinterpret_cast<char*>(bgr.data()), (std::streamsize)(bgr.size() * 3));
+    for (auto& p : bgr) std::swap(p.x, p.z);                           // RGB on disk -> BGR (imread order)
+    sm::Mat gray(h, w);
+    auto t0 = std::chrono::steady_clock::now();
+    cvtColor_gpu(bgr.data(), gray.data, h, w);
+    auto t1 = std::chrono::steady_clock::now();
+    std::cout << "GPU cvtColor : " << std::chrono::duration<double, std::milli>(t1 - t0).count() << std::endl;
+    write_pgm(env_or("SM_OUT", "gray.pgm"), gray);
+}

@@ -1,12 +1,17 @@
 // Main.cpp — the reference's entry point (BlockMatching/Main.cpp:3-9), unchanged in shape.
+// SM_DEMO selects which Caller.h demo runs: singleFrame (default), remapTest or cvtColorTest.
 #include <cstdlib>
+#include <cstring>
 #include "Caller.h"
 
 int main() {
-    singleFrame();
-    if (std::getenv("SM_ALL_DEMOS")) {
+    const char* demo = std::getenv("SM_DEMO");
+    if (demo && std::strcmp(demo, "remapTest") == 0) {
         remapTest();
+    } else if (demo && std::strcmp(demo, "cvtColorTest") == 0) {
         cvtColorTest();
+    } else {
+        singleFrame();
     }
     return 0;
 }

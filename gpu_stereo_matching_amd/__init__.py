@@ -126,6 +126,29 @@ class BlockMatcher:
                                                     num_disp, _flags(agg, lr_check), out.ctypes.data, W))
         return out
 
+    def cvt_color(self, bgr) -> np.ndarray:
+        """cvtColor_gpu (Device.cuh:52) on host memory: HxWx3|4 uint8 BGR(A) -> gray, OpenCV 2.4 weights."""
+        B = np.ascontiguousarray(bgr, dtype=np.uint8)
+        if B.ndim != 3 or B.shape[2] not in (3, 4):
+            raise ValueError("expected an HxWx3 or HxWx4 uint8 BGR(A) image")
+        H, W, C = B.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_bgr_to_gray_u8(self._h, B.ctypes.data, W, H, W * C, C, out.ctypes.data, W))
+        return out
+
+    def remap(self, src, mapx, mapy) -> np.ndarray:
+        """remap_gpu (Device.cuh:51) on host memory: uint8 [H, W] with CV_32FC1 maps [H, W]."""
+        S = _as_u8_image(src, "src")
+        mx = np.ascontiguousarray(mapx, dtype=np.float32)
+        my = np.ascontiguousarray(mapy, dtype=np.float32)
+        if mx.shape != S.shape or my.shape != S.shape:
+            raise ValueError("maps must match the image shape")
+        H, W = S.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_remap_u8(self._h, S.ctypes.data, W, H, W, mx.ctypes.data, my.ctypes.data, W,
+                                          out.ctypes.data, W))
+        return out
+
     def bgr_to_gray_device(self, bgr_t, out_t=None, stream=None):
         """[H, W, 3|4] uint8 cuda tensor -> [H, W] gray (OpenCV 2.4 fixed point), async on `stream`."""
         import torch

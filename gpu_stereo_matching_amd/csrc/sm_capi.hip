@@ -28,6 +28,9 @@ struct sm_handle {
     // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
     uint8_t* d_lr = nullptr;
     size_t lr_bytes = 0;
+    // float maps of the host remap entry point (grown on demand)
+    float* d_maps = nullptr;
+    size_t maps_bytes = 0;
     // right-map / mask staging of the host LR entry point (grown on demand)
     uint8_t* d_aux = nullptr;
     size_t aux_bytes = 0;
@@ -309,6 +312,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_lr);
     (void)hipFree(h->d_rpart);
     (void)hipFree(h->d_aux);
+    (void)hipFree(h->d_maps);
     (void)hipFree(h->d_bgr);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -424,6 +428,61 @@ SM_API int sm_remap_u8_device(sm_handle* h, const uint8_t* d_src, int width, int
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(sm::launch_remap(d_src, width, height, pitch, d_mapx, d_mapy, map_pitch, d_dst, dst_pitch,
                             (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_bgr_to_gray_u8(sm_handle* h, const uint8_t* bgr, int width, int height, int pitch, int channels,
+                             uint8_t* gray, int gray_pitch) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!bgr || !gray || width <= 0 || height <= 0 || (channels != 3 && channels != 4) || pitch < width * channels ||
+        gray_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad BGR layout");
+    if (width > h->max_w || height > h->max_h) return fail(SM_ERR_CAPACITY, "frame exceeds handle capacity");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t need = (size_t)width * channels * height;
+    if (h->bgr_bytes < need) {
+        if (h->d_bgr) (void)hipFree(h->d_bgr);
+        h->d_bgr = nullptr;
+        h->bgr_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_bgr, need));
+        h->bgr_bytes = need;
+    }
+    SM_HIP(hipMemcpy2DAsync(h->d_bgr, (size_t)width * channels, bgr, pitch, (size_t)width * channels, height,
+                            hipMemcpyHostToDevice, s));
+    SM_HIP(sm::launch_bgr_to_gray(h->d_bgr, width, height, width * channels, channels, h->d_left, width, s));
+    SM_HIP(hipMemcpy2DAsync(gray, gray_pitch, h->d_left, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
+}
+
+SM_API int sm_remap_u8(sm_handle* h, const uint8_t* src, int width, int height, int pitch, const float* mapx,
+                       const float* mapy, int map_pitch, uint8_t* dst, int dst_pitch) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!src || !mapx || !mapy || !dst || width <= 0 || height <= 0 || pitch < width || map_pitch < width ||
+        dst_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad remap arguments");
+    if (width > h->max_w || height > h->max_h) return fail(SM_ERR_CAPACITY, "frame exceeds handle capacity");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t plane = (size_t)width * height;
+    if (h->maps_bytes < 2 * plane * sizeof(float)) {
+        if (h->d_maps) (void)hipFree(h->d_maps);
+        h->d_maps = nullptr;
+        h->maps_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_maps, 2 * plane * sizeof(float)));
+        h->maps_bytes = 2 * plane * sizeof(float);
+    }
+    float* dmx = h->d_maps;
+    float* dmy = h->d_maps + plane;
+    SM_HIP(hipMemcpy2DAsync(dmx, width * sizeof(float), mapx, (size_t)map_pitch * sizeof(float), width * sizeof(float),
+                            height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipMemcpy2DAsync(dmy, width * sizeof(float), mapy, (size_t)map_pitch * sizeof(float), width * sizeof(float),
+                            height, hipMemcpyHostToDevice, s));
+    SM_HIP(hipMemcpy2DAsync(h->d_left, width, src, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(sm::launch_remap(h->d_left, width, height, width, dmx, dmy, width, h->d_right, width, s));
+    SM_HIP(hipMemcpy2DAsync(dst, dst_pitch, h->d_right, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
 }
 

@@ -134,6 +134,13 @@ SM_API int sm_remap_u8_device(sm_handle *h, const uint8_t *d_src, int width, int
 SM_API int sm_median_u8_device(sm_handle *h, const uint8_t *d_src, int width, int height, int pitch,
                                int radius, uint8_t *d_dst, int dst_pitch, void *stream);
 
+/* Host-pointer, synchronous forms of the two steps above (the reference's cvtColor_gpu /
+ * remap_gpu, Device.cuh:51-52).  Buffers are staged through the handle. */
+SM_API int sm_bgr_to_gray_u8(sm_handle *h, const uint8_t *bgr, int width, int height, int pitch, int channels,
+                             uint8_t *gray, int gray_pitch);
+SM_API int sm_remap_u8(sm_handle *h, const uint8_t *src, int width, int height, int pitch, const float *mapx,
+                       const float *mapy, int map_pitch, uint8_t *dst, int dst_pitch);
+
 /* imread -> cvtColor -> blockMatching_gpu in one call (Caller.cpp:12-19): BGR(A) host frames
  * are uploaded, converted to gray on the GPU and matched.  Synchronous. */
 SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,

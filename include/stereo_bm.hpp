@@ -1,8 +1,13 @@
-// stereo_bm.hpp — header-only C++ adapter that keeps the reference's host API
+// stereo_bm.hpp — header-only C++ adapter that keeps the reference's host API (Device.cuh:50-52)
 //   void blockMatching_gpu(Mat &h_left, Mat &h_right, Mat &h_disparity,
-//                          int SADWindowSize, int searchRange);          // Device.cuh:50
-// on top of the C ABI in sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame) shaped caller
-// compiles and runs unchanged apart from the include.
+//                          int SADWindowSize, int searchRange);
+//   void remap_gpu(Mat &left, Mat &right, Mat &mapX1, Mat &mapY1, Mat &mapX2, Mat &mapY2,
+//                  int rows, int cols, int total, uchar *result);
+//   void cvtColor_gpu(uchar3 *src, uchar *dst, int rows, int cols);
+// on top of the C ABI in sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame, remapTest,
+// cvtColorTest) shaped caller compiles and runs unchanged apart from the include.  Host-only:
+// compile it with a plain C++ compiler (it declares the host type uchar3 the reference's callers
+// cast to).
 //
 // Works with cv::Mat when OpenCV is available (define SM_WITH_OPENCV before including, after
 // including <opencv2/core/core.hpp>), and with the minimal sm::Mat below otherwise (this image
@@ -30,27 +35,43 @@
 #ifndef CV_8UC1
 #define CV_8UC1 0
 #endif
+#ifndef CV_32FC1
+#define CV_32FC1 5
+#endif
+
+// the host vector type the reference's callers cast BGR data to (Caller.cpp:92, Device.cuh:52)
+struct uchar3 {
+    unsigned char x, y, z;
+};
+typedef unsigned char uchar;
 
 namespace sm {
 
-// Minimal single-channel 8-bit image (the subset of cv::Mat that the reference's path uses).
+// Minimal single-channel image (the subset of cv::Mat that the reference's path uses): 8-bit by
+// default, or CV_32FC1 for remap maps (elem = 4).
 struct Mat {
     int rows = 0, cols = 0;
     size_t step = 0;                     // bytes per row
+    size_t elem = 1;                     // bytes per element (1: CV_8UC1, 4: CV_32FC1)
     uint8_t* data = nullptr;
     std::shared_ptr<std::vector<uint8_t>> store;
 
     Mat() = default;
     Mat(int r, int c, int type = CV_8UC1) { create(r, c, type); }
     // wrap external memory (not owned), like cv::Mat(rows, cols, CV_8UC1, ptr)
-    Mat(int r, int c, int /*type*/, void* ptr, size_t stp = 0)
-        : rows(r), cols(c), step(stp ? stp : (size_t)c), data(static_cast<uint8_t*>(ptr)) {}
-    void create(int r, int c, int /*type*/ = CV_8UC1) {
-        if (r == rows && c == cols && store) return;
+    Mat(int r, int c, int type, void* ptr, size_t stp = 0)
+        : rows(r), cols(c), elem(elem_size(type)), data(static_cast<uint8_t*>(ptr)) {
+        step = stp ? stp : (size_t)c * elem;
+    }
+    static size_t elem_size(int type) { return type == CV_32FC1 ? 4 : 1; }
+    void create(int r, int c, int type = CV_8UC1) {
+        const size_t e = elem_size(type);
+        if (r == rows && c == cols && e == elem && store) return;
         rows = r;
         cols = c;
-        step = (size_t)c;
-        store = std::make_shared<std::vector<uint8_t>>((size_t)r * c, 0);
+        elem = e;
+        step = (size_t)c * e;
+        store = std::make_shared<std::vector<uint8_t>>((size_t)r * step, 0);
         data = store->data();
     }
     template <typename T> T* ptr(int r = 0) { return reinterpret_cast<T*>(data + (size_t)r * step); }
@@ -124,17 +145,50 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     return rc;
 }
 
+// remap_gpu (Device.cu:303-342): both views rectified on the GPU; `result` receives the left
+// view (the reference copies back only d_left_gpu_data, :341).  Maps are CV_32FC1.
+template <typename M, typename F>
+inline int remap(const M& left, const M& right, const F& mapX1, const F& mapY1, const F& mapX2, const F& mapY2,
+                 int rows, int cols, uint8_t* result, uint8_t* right_result = nullptr) {
+    detail::Engine& e = detail::engine();
+    if (!e.ensure(cols, rows, 1)) return SM_ERR_DEVICE;
+    const int mp = (int)(detail::row_step(mapX1) / sizeof(float));
+    int rc = sm_remap_u8(e.h, left.data, cols, rows, (int)detail::row_step(left),
+                         reinterpret_cast<const float*>(mapX1.data), reinterpret_cast<const float*>(mapY1.data), mp,
+                         result, cols);
+    if (rc == SM_OK && right_result)
+        rc = sm_remap_u8(e.h, right.data, cols, rows, (int)detail::row_step(right),
+                         reinterpret_cast<const float*>(mapX2.data), reinterpret_cast<const float*>(mapY2.data),
+                         (int)(detail::row_step(mapX2) / sizeof(float)), right_result, cols);
+    if (rc != SM_OK) std::cerr << "remap_gpu: " << sm_last_error_string() << std::endl;
+    return rc;
+}
+
 }  // namespace sm
 
-// ---- the reference's free function, unchanged signature (Device.cuh:50) ----
+// ---- the reference's free functions, unchanged signatures (Device.cuh:50-52) ----
+
+// BGR -> gray of a rows x cols packed uchar3 image.  Computes what the reference's callers use,
+// OpenCV 2.4 cvtColor(CV_BGR2GRAY) (Y = (1868 B + 9617 G + 4899 R + 8192) >> 14); the
+// reference's own kernalCvtColor applies the luma weights to B,G,R swapped (Device.cu:136-143)
+// and is deliberately not reproduced.
+inline void cvtColor_gpu(uchar3* src, uchar* dst, int rows, int cols) {
+    sm::detail::Engine& e = sm::detail::engine();
+    if (!e.ensure(cols, rows, 1)) return;
+    if (sm_bgr_to_gray_u8(e.h, reinterpret_cast<const uint8_t*>(src), cols, rows, cols * 3, 3, dst, cols) != SM_OK)
+        std::cerr << "cvtColor_gpu: " << sm_last_error_string() << std::endl;
+}
+
 #ifdef SM_WITH_OPENCV
-inline void blockMatching_gpu(cv::Mat& h_left, cv::Mat& h_right, cv::Mat& h_disparity, int SADWindowSize,
-                              int searchRange) {
-    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange);
-}
+using SmHostMat = cv::Mat;
 #else
-inline void blockMatching_gpu(sm::Mat& h_left, sm::Mat& h_right, sm::Mat& h_disparity, int SADWindowSize,
+using SmHostMat = sm::Mat;
+#endif
+inline void blockMatching_gpu(SmHostMat& h_left, SmHostMat& h_right, SmHostMat& h_disparity, int SADWindowSize,
                               int searchRange) {
     sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange);
 }
-#endif
+inline void remap_gpu(SmHostMat& left, SmHostMat& right, SmHostMat& mapX1, SmHostMat& mapY1, SmHostMat& mapX2,
+                      SmHostMat& mapY2, int rows, int cols, int /*total*/, uchar* result) {
+    sm::remap(left, right, mapX1, mapY1, mapX2, mapY2, rows, cols, result);
+}

@@ -40,3 +40,39 @@ def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):
     assert "GPU : " in r.stdout and "find corr : " in r.stdout
     got = _read_pgm(tmp_path / "d.pgm")
     assert np.array_equal(got, bm_expected[f"{pair}/r{sad}/D{rng}"])
+
+
+@pytest.mark.gpu
+def test_remap_test_cpp(tmp_path, gray, oracle):
+    """remapTest() -> remap_gpu(Mat&...) (Device.cuh:51) against the CPU_Remap restatement."""
+    L, R = gray["Art/view1"], gray["Art/view5"]
+    H, W = L.shape
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    th = np.float32(0.03)
+    mapx = (np.cos(th) * xx - np.sin(th) * yy + np.float32(3.25)).astype(np.float32)
+    mapy = (np.sin(th) * xx + np.cos(th) * yy - np.float32(7.5)).astype(np.float32)
+    _write_pgm(tmp_path / "l.pgm", L)
+    _write_pgm(tmp_path / "r.pgm", R)
+    mapx.tofile(tmp_path / "mx.f32")
+    mapy.tofile(tmp_path / "my.f32")
+    env = dict(os.environ, SM_DEMO="remapTest", SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
+               SM_MAPX=str(tmp_path / "mx.f32"), SM_MAPY=str(tmp_path / "my.f32"), SM_OUT=str(tmp_path / "o.pgm"))
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "GPU Remap : " in r.stdout
+    assert np.array_equal(_read_pgm(tmp_path / "o.pgm"), oracle.remap(L, mapx, mapy))
+
+
+@pytest.mark.gpu
+def test_cvtcolor_test_cpp(tmp_path, gray, oracle):
+    """cvtColorTest() -> cvtColor_gpu(uchar3*...) (Device.cuh:52): OpenCV 2.4 BGR2GRAY, bit-exact."""
+    bgr = gray["Art_/view1_bgr"]
+    with open(tmp_path / "c.ppm", "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (bgr.shape[1], bgr.shape[0]))
+        f.write(np.ascontiguousarray(bgr[..., ::-1]).tobytes())        # RGB on disk
+    env = dict(os.environ, SM_DEMO="cvtColorTest", SM_BGR=str(tmp_path / "c.ppm"), SM_OUT=str(tmp_path / "g.pgm"))
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = _read_pgm(tmp_path / "g.pgm")
+    assert np.array_equal(got, oracle.bgr_to_gray(bgr))
+    assert np.array_equal(got, gray["Art_/view1"])

@@ -93,3 +93,19 @@ def test_gpu_remap(oracle, kind):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), oracle.remap(src, mx, my))
     m.close()
+
+
+@pytest.mark.gpu
+def test_host_entry_points_cvt_color_and_remap(oracle, gray):
+    """sm_bgr_to_gray_u8 / sm_remap_u8: the host-pointer forms behind cvtColor_gpu / remap_gpu."""
+    import gpu_stereo_matching_amd as sm
+    m = sm.BlockMatcher(0, 640, 480, 64)
+    bgr = gray["Art_/view1_bgr"]
+    assert np.array_equal(m.cvt_color(bgr), oracle.bgr_to_gray(bgr))
+    L = gray["Art/view1"]
+    H, W = L.shape
+    rng = np.random.default_rng(5)
+    mapx = (np.arange(W, dtype=np.float32)[None, :] + rng.uniform(-3, 3, (H, W)).astype(np.float32))
+    mapy = (np.arange(H, dtype=np.float32)[:, None] + rng.uniform(-3, 3, (H, W)).astype(np.float32))
+    assert np.array_equal(m.remap(L, mapx, mapy), oracle.remap(L, mapx, mapy))
+    m.close()
