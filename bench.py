@@ -118,6 +118,20 @@ def run_variants(sm, torch, dev, stream, seed):
                 out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": B}
             except Exception as e:  # report, never hide
                 out[name] = {"error": str(e)}
+        # the drop-in host path (sm_block_match_u8: pageable H2D, match, D2H), PCIe-inclusive
+        for (name, W, H, D, r) in (("host round trip 1080p 11x11 box d128", 1920, 1080, 128, 5),
+                                   ("host round trip 463x370 9x9 box d64", 463, 370, 64, 4)):
+            L, R = sm.synth_pair(seed, W, H, D)
+            for _ in range(3):
+                m.match(L, R, r, D)
+            n = 20
+            t0 = time.perf_counter()
+            for _ in range(n):
+                m.match(L, R, r, D)
+            ms = (time.perf_counter() - t0) * 1000 / n
+            up, mt, dn = m.stage_ms()
+            out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
+                         "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
     finally:
         m.close()
     return out

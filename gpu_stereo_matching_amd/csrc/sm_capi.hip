@@ -12,6 +12,7 @@
 #include <cstring>
 #include <cstdarg>
 #include <new>
+#include <vector>
 
 #include "../../include/sm_hip.h"
 #include "bm_common.h"
@@ -101,6 +102,35 @@ int ensure_rpart(sm_handle* h, size_t bytes) {
     SM_HIP(hipMalloc(&h->d_rpart, bytes));
     h->rpart_bytes = bytes;
     return SM_OK;
+}
+
+// Host<->device 2-D copy.  Contiguous rows (both pitches == row bytes) go as one 1-D copy: the
+// 2-D path takes a slow per-row route for widths that are not a multiple of 4 (measured 5.7 ms
+// instead of 0.02 ms to upload a 463x370 pair).
+// Pitched host buffers are gathered into / scattered from a contiguous host vector around one
+// 1-D copy (the pageable 2-D path is the slow one, pitched or not).
+thread_local std::vector<uint8_t> g_host_rows;
+
+hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t row_bytes, size_t rows,
+                  hipMemcpyKind kind, hipStream_t s) {
+    if (dpitch == row_bytes && spitch == row_bytes) return hipMemcpyAsync(dst, src, row_bytes * rows, kind, s);
+    if (kind == hipMemcpyHostToDevice && dpitch == row_bytes) {
+        g_host_rows.resize(row_bytes * rows);
+        for (size_t r = 0; r < rows; ++r)
+            std::memcpy(g_host_rows.data() + r * row_bytes, static_cast<const uint8_t*>(src) + r * spitch, row_bytes);
+        // a pageable source is staged before the call returns, so the vector may be reused
+        return hipMemcpyAsync(dst, g_host_rows.data(), row_bytes * rows, kind, s);
+    }
+    if (kind == hipMemcpyDeviceToHost && spitch == row_bytes) {
+        g_host_rows.resize(row_bytes * rows);
+        hipError_t e = hipMemcpyAsync(g_host_rows.data(), src, row_bytes * rows, kind, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        for (size_t r = 0; r < rows; ++r)
+            std::memcpy(static_cast<uint8_t*>(dst) + r * dpitch, g_host_rows.data() + r * row_bytes, row_bytes);
+        return hipSuccess;
+    }
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, row_bytes, rows, kind, s);
 }
 
 // Core device-side pass over `batch` frames.  Workspace planes (d_lr) are dense W x H frames.
@@ -233,16 +263,16 @@ int host_match(sm_handle* h, const uint8_t* left, const uint8_t* right, int widt
         aux = h->d_aux;
     }
     SM_HIP(hipEventRecord(h->ev[0], s));
-    SM_HIP(hipMemcpy2DAsync(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
-    SM_HIP(hipMemcpy2DAsync(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(hipEventRecord(h->ev[1], s));
     rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
                     right_out ? aux : nullptr, mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
     SM_HIP(hipEventRecord(h->ev[2], s));
-    SM_HIP(hipMemcpy2DAsync(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
-    if (right_out) SM_HIP(hipMemcpy2DAsync(right_out, out_pitch, aux, width, width, height, hipMemcpyDeviceToHost, s));
-    if (mask_out) SM_HIP(hipMemcpy2DAsync(mask_out, out_pitch, aux + P, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
+    if (right_out) SM_HIP(copy2d(right_out, out_pitch, aux, width, width, height, hipMemcpyDeviceToHost, s));
+    if (mask_out) SM_HIP(copy2d(mask_out, out_pitch, aux + P, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
     SM_HIP(hipEventSynchronize(h->ev[3]));
     SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
@@ -448,10 +478,10 @@ SM_API int sm_bgr_to_gray_u8(sm_handle* h, const uint8_t* bgr, int width, int he
         SM_HIP(hipMalloc(&h->d_bgr, need));
         h->bgr_bytes = need;
     }
-    SM_HIP(hipMemcpy2DAsync(h->d_bgr, (size_t)width * channels, bgr, pitch, (size_t)width * channels, height,
+    SM_HIP(copy2d(h->d_bgr, (size_t)width * channels, bgr, pitch, (size_t)width * channels, height,
                             hipMemcpyHostToDevice, s));
     SM_HIP(sm::launch_bgr_to_gray(h->d_bgr, width, height, width * channels, channels, h->d_left, width, s));
-    SM_HIP(hipMemcpy2DAsync(gray, gray_pitch, h->d_left, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(copy2d(gray, gray_pitch, h->d_left, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
 }
@@ -475,13 +505,13 @@ SM_API int sm_remap_u8(sm_handle* h, const uint8_t* src, int width, int height, 
     }
     float* dmx = h->d_maps;
     float* dmy = h->d_maps + plane;
-    SM_HIP(hipMemcpy2DAsync(dmx, width * sizeof(float), mapx, (size_t)map_pitch * sizeof(float), width * sizeof(float),
+    SM_HIP(copy2d(dmx, width * sizeof(float), mapx, (size_t)map_pitch * sizeof(float), width * sizeof(float),
                             height, hipMemcpyHostToDevice, s));
-    SM_HIP(hipMemcpy2DAsync(dmy, width * sizeof(float), mapy, (size_t)map_pitch * sizeof(float), width * sizeof(float),
+    SM_HIP(copy2d(dmy, width * sizeof(float), mapy, (size_t)map_pitch * sizeof(float), width * sizeof(float),
                             height, hipMemcpyHostToDevice, s));
-    SM_HIP(hipMemcpy2DAsync(h->d_left, width, src, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_left, width, src, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(sm::launch_remap(h->d_left, width, height, width, dmx, dmy, width, h->d_right, width, s));
-    SM_HIP(hipMemcpy2DAsync(dst, dst_pitch, h->d_right, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(copy2d(dst, dst_pitch, h->d_right, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
 }
@@ -522,8 +552,8 @@ SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const ui
     uint8_t* dr = h->d_bgr + row * height;
     const int64_t P = (int64_t)width * height;
     SM_HIP(hipEventRecord(h->ev[0], s));
-    SM_HIP(hipMemcpy2DAsync(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
-    SM_HIP(hipMemcpy2DAsync(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
     SM_HIP(hipEventRecord(h->ev[1], s));
     SM_HIP(sm::launch_bgr_to_gray(dl, width, height, (int)row, channels, h->d_left, width, s));
     SM_HIP(sm::launch_bgr_to_gray(dr, width, height, (int)row, channels, h->d_right, width, s));
@@ -531,7 +561,7 @@ SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const ui
                     nullptr, nullptr, width, P, s);
     if (rc) return rc;
     SM_HIP(hipEventRecord(h->ev[2], s));
-    SM_HIP(hipMemcpy2DAsync(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
     SM_HIP(hipEventSynchronize(h->ev[3]));
     SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
