@@ -76,11 +76,7 @@ struct Geo {
     static constexpr int PW = TW + DMAX + 1;                    // partial row width written to HBM
     static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
     static constexpr int RB_BYTES = kTileH * RBW * 4;
-#if SM_ABLATE & 32
-    static constexpr int LDS_BYTES_R = LDS_BYTES;
-#else
     static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
-#endif
     static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
 };
 
@@ -124,11 +120,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                     // [NW][HALF][CSS]
     uint16_t* rs = reinterpret_cast<uint16_t*>(smem + G::FRONT);          // [ROWS][RW]
-#if SM_ABLATE & 32
-    uint32_t* rb = reinterpret_cast<uint32_t*>(smem);
-#else
     uint32_t* rb = reinterpret_cast<uint32_t*>(smem + G::FRONT + G::RS_BYTES);  // RIGHT: [kTileH][RBW]
-#endif
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -350,9 +342,6 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     }
     __syncthreads();
 
-#if SM_ABLATE & 4
-    if (a.W > 0) { if (tid == 0) a.disp[0] = (uint8_t)(best[0][0] ^ best[1][G::NQ - 1]); return; }
-#endif
     // ---- fold the NW waves (same lane = same pixels in every wave) through one LDS plane ----
     uint32_t* fold = cs;                                   // [kTileH][TW] keys
     if (wave == 0) {

@@ -1,4 +1,5 @@
-"""Time the box kernel from an ablation build of libsm_hip.so (path as argv[1])."""
+"""Time one libsm_hip.so build (path as argv[1]) on the 1080p D=128 workload; env SM_AB_R / SM_AB_D /
+SM_AB_B / SM_AB_LR / SM_AB_AGG select radius, disparities, frames per call, LR and aggregation."""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
