@@ -256,3 +256,46 @@ def test_stage_timings(matcher, gray):
     matcher.match(gray["Art_/view1"], gray["Art_/view5"], 5, 64)
     u, c, d = matcher.stage_ms()
     assert u > 0 and c > 0 and d > 0
+
+
+def test_frame_stream_pipeline(matcher, oracle, torch):
+    """FrameStream (copy/compute overlap on two streams, double-buffered pinned slots) returns every
+    batch, in order, identical to the oracle."""
+    from gpu_stereo_matching_amd.pipeline import FrameStream
+    B, W, H, D, r = 3, 200, 64, 32, 3
+    fs = FrameStream(matcher, B, W, H, r, D)
+    batches, outs = [], []
+    for k in range(5):
+        pairs = [oracle.synth_pair(100 * k + i, W, H, D) for i in range(B)]
+        Ls, Rs = np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])
+        batches.append((Ls, Rs))
+        if k % 2:
+            l_view, r_view = fs.next_inputs()           # in-place producer path
+            l_view[...] = Ls
+            r_view[...] = Rs
+            outs += fs.submit()
+        else:
+            outs += fs.submit(Ls, Rs)
+    outs += fs.flush()
+    assert len(outs) == 5
+    for (Ls, Rs), got in zip(batches, outs):
+        for i in range(B):
+            assert np.array_equal(got[i], oracle.box_disp(Ls[i], Rs[i], r, D))
+
+
+def test_frame_stream_consume_callback(matcher, oracle):
+    from gpu_stereo_matching_amd.pipeline import FrameStream
+    B, W, H, D, r = 2, 96, 40, 16, 2
+    seen = []
+    fs = FrameStream(matcher, B, W, H, r, D, consume=lambda disp: seen.append(disp.copy()))
+    batches = []
+    for k in range(4):
+        pairs = [oracle.synth_pair(7 * k + i, W, H, D) for i in range(B)]
+        Ls, Rs = np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])
+        batches.append((Ls, Rs))
+        assert fs.submit(Ls, Rs) == []
+    assert fs.flush() == []
+    assert len(seen) == 4
+    for (Ls, Rs), got in zip(batches, seen):
+        for i in range(B):
+            assert np.array_equal(got[i], oracle.box_disp(Ls[i], Rs[i], r, D))
