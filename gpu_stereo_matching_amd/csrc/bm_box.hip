@@ -55,11 +55,13 @@ struct Geo {
     static constexpr int NQ = (((TW + 3) / 4) + 1) & ~1;        // outputs per phase-H thread (even: b64 reads)
     static constexpr int NCS2 = (NQ + 2 * R + 1) / 2;           // 8-B CS reads per phase-H thread
     static constexpr int NEED = 3 * NQ + 2 * NCS2;              // last CS column read + 1
-    // row stride in dwords: for NQ == 2 (mod 4) a stride == 4 (mod 8) puts the 32 lanes of a
-    // ds_read_b64 group (16 rows x 2 quarters) on 64 distinct banks; for NQ == 16 no stride is
-    // conflict-free; the smallest even one that is not a multiple of 32 is 2-way
+    // row stride in dwords, chosen by measurement on MI355X (32 x 1080p frames, D = 128):
+    //   NQ = 14 (r >= 4): the smallest >= NEED with stride == 2 (mod 4); at r = 5, 66 / 70 run
+    //     56.1 us/frame against 58.7 for 68 / 76 / 84, 76.5 for 72 and 124.3 for 80 (r = 4, 6, 7
+    //     gain 3.5-6 % over the old == 4 (mod 8) rule);
+    //   NQ = 16 (r <= 3): the smallest even stride that is not a multiple of 32.
     static constexpr int CSS_EVEN = (NEED + 1) & ~1;
-    static constexpr int CSS = (NQ % 4 == 2) ? (NEED + ((12 - NEED % 8) % 8))
+    static constexpr int CSS = (NQ % 4 == 2) ? NEED + ((6 - NEED % 4) % 4)
                                              : (CSS_EVEN % 32 == 0 ? CSS_EVEN + 2 : CSS_EVEN);
     static constexpr int CS_BYTES = NW * HALF * CSS * 4;        // NW waves x one half-tile plane
     static constexpr int RW = kCols + DMAX + 4;                 // u16 entries per right-band row (x4-aligned base)
