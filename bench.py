@@ -132,7 +132,7 @@ def run_variants(sm, torch, dev, stream, seed):
             rv[...] = Rs
             fs.submit()
         fs.flush()
-        nb = 24
+        nb = 48
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for k in range(nb):

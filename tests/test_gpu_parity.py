@@ -252,6 +252,30 @@ def test_error_codes(sm, matcher):
     small.close()
 
 
+def test_error_codes_side_entries(sm, torch):
+    """Argument and capacity checks of the non-matching entry points, and recovery afterwards."""
+    small = sm.BlockMatcher(0, 32, 16, 32)
+    with pytest.raises(sm.SMError) as e:                       # capacity
+        small.cvt_color(np.zeros((17, 32, 3), np.uint8))
+    assert e.value.code == 5
+    with pytest.raises(sm.SMError) as e:
+        small.remap(np.zeros((16, 33), np.uint8), np.zeros((16, 33), np.float32), np.zeros((16, 33), np.float32))
+    assert e.value.code == 5
+    x = torch.zeros((8, 8), dtype=torch.uint8, device="cuda")
+    for bad_r in (0, 4):
+        with pytest.raises(sm.SMError) as e:
+            small.median_device(x, bad_r)
+        assert e.value.code == 1
+    lib = small._lib
+    assert lib.sm_median_u8_device(small._h, None, 8, 8, 8, 1, x.data_ptr(), 8, None) == 1
+    assert lib.sm_remap_u8(small._h, None, 8, 8, 8, None, None, 8, None, 8) == 1
+    assert b"remap" in lib.sm_last_error_string()
+    # the handle still works after the failures
+    L = np.random.default_rng(0).integers(0, 256, (16, 32), dtype=np.uint8)
+    assert small.match(L, L, 1, 8).shape == (16, 32)
+    small.close()
+
+
 def test_stage_timings(matcher, gray):
     matcher.match(gray["Art_/view1"], gray["Art_/view5"], 5, 64)
     u, c, d = matcher.stage_ms()
