@@ -118,6 +118,25 @@ def run_variants(sm, torch, dev, stream, seed):
                 out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": B}
             except Exception as e:  # report, never hide
                 out[name] = {"error": str(e)}
+        # row a1 on its own: the AD volume (PreCal / kernalPreCal_V2), an HBM-write-bound kernel
+        W, H, D = 1920, 1080, 128
+        L, R = sm.synth_pair(seed, W, H, D)
+        Lt, Rt = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+        vol = torch.empty((D, H, W), dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            m.ad_volume_device(Lt, Rt, D, out_t=vol, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            m.ad_volume_device(Lt, Rt, D, out_t=vol, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / 20
+        gbs = W * H * (D + 2) / (ms * 1e-3) / 1e9
+        out["a1 AD volume 1080p d128 (PreCal, HBM-write-bound)"] = {
+            "ms_per_frame": round(ms, 4), "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 3),
+            "bytes_per_frame": W * H * (D + 2)}
+        del vol
         # host frame stream, PCIe-inclusive: FrameStream overlaps H2D / match / D2H on three streams;
         # frames are produced in place in the pinned slots (next_inputs) and consumed in place
         # (callback), so no host-side copy is timed

@@ -108,3 +108,25 @@ void cvtColorTest() {
     std::cout << "GPU cvtColor : " << std::chrono::duration<double, std::milli>(t1 - t0).count() << std::endl;
     write_pgm(env_or("SM_OUT", "gray.pgm"), gray);
 }
+
+// Not a reference demo: BlockMatching.h's testBM / getDisp / PreCal through the adapter (the
+// reference uses them to cross-check its GPU path, BlockMatching.cpp:263-308).  Writes the
+// testBM and getDisp maps (PGM) and the AD volume (raw, D planes).
+void blockMatchingApiTest() {
+    sm::Mat g1, g2, disp;
+    if (!read_pgm(env_or("SM_LEFT", "view1_.pgm"), g1) || !read_pgm(env_or("SM_RIGHT", "view5_.pgm"), g2)) {
+        std::cerr << "cannot read the pair" << std::endl;
+        std::exit(2);
+    }
+    const int sad = std::atoi(env_or("SM_SAD", "5").c_str());
+    const int range = std::atoi(env_or("SM_RANGE", "64").c_str());
+    testBM(g1, g2, disp, sad, range);
+    write_pgm(env_or("SM_OUT", "disp.pgm"), disp);
+    sm::Mat disp2(g1.rows, g1.cols);
+    getDisp(g1, g2, disp2.data, sad, range);
+    write_pgm(env_or("SM_OUT2", "disp2.pgm"), disp2);
+    std::vector<uchar> dif((size_t)g1.rows * g1.cols * range, 0);
+    PreCal(g1, g2, dif.data(), sad, range);
+    std::ofstream f(env_or("SM_VOL", "dif.u8"), std::ios::binary);
+    f.write(reinterpret_cast<const char*>(dif.data()), (std::streamsize)dif.size());
+}

@@ -3,3 +3,4 @@
 void singleFrame();
 void remapTest();
 void cvtColorTest();
+void blockMatchingApiTest();   // not in the reference's Caller.h: BlockMatching.h through the adapter

@@ -10,6 +10,8 @@ int main() {
         remapTest();
     } else if (demo && std::strcmp(demo, "cvtColorTest") == 0) {
         cvtColorTest();
+    } else if (demo && std::strcmp(demo, "blockMatchingApiTest") == 0) {
+        blockMatchingApiTest();
     } else {
         singleFrame();
     }

@@ -149,6 +149,25 @@ class BlockMatcher:
                                           out.ctypes.data, W))
         return out
 
+    def ad_volume(self, left, right, num_disp: int) -> np.ndarray:
+        """PreCal (BlockMatching.cpp:89-109) on the GPU: uint8 [num_disp, H, W], d-major, 0 where x < d."""
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        H, W = L.shape
+        out = np.empty((num_disp, H, W), np.uint8)
+        _capi.check(self._lib.sm_ad_volume_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, num_disp,
+                                              out.ctypes.data))
+        return out
+
+    def ad_volume_device(self, left_t, right_t, num_disp: int, out_t=None, stream=None):
+        import torch
+        H, W = left_t.shape
+        if out_t is None:
+            out_t = torch.empty((num_disp, H, W), dtype=torch.uint8, device=left_t.device)
+        _capi.check(self._lib.sm_ad_volume_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, num_disp,
+                                                  out_t.data_ptr(), self._stream_ptr(stream)))
+        return out_t
+
     def bgr_to_gray_device(self, bgr_t, out_t=None, stream=None):
         """[H, W, 3|4] uint8 cuda tensor -> [H, W] gray (OpenCV 2.4 fixed point), async on `stream`."""
         import torch

@@ -55,6 +55,9 @@ hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride
                            int W, int H, int batch, uint8_t* out, int opitch, int64_t ostride,
                            uint8_t* right_out, uint8_t* mask_out, int aux_pitch, int64_t aux_stride,
                            hipStream_t s);
+// AD volume dif[d][y][x] (PreCal / kernalPreCal_V2), d-major planes per frame (bm_volume.hip)
+hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int64_t fstride, int batch,
+                            int D, uint8_t* dif, int64_t dstride, hipStream_t s);
 // (2r+1)^2 median with replicate borders, radius 1..3 (bm_post.hip)
 hipError_t launch_median(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch, int radius,
                          uint8_t* dst, int dpitch, int64_t dstride, hipStream_t s);

@@ -1,0 +1,125 @@
+// bm_volume.hip — the absolute-difference cost volume itself, for callers of the
+// reference's PreCal (BlockMatching.cpp:89-109) / kernalPreCal_V2 (Device.cu:19-32):
+//   dif[d][y][x] = |L(y,x) - R(y,x-d)|  for x >= d,  0 otherwise (the memset, Device.cu:194),
+// d-major planes [D][H][W] exactly as Device.cu:193 lays them out.  The matching path never
+// builds this volume (it is fused into box_match_kernel); this kernel exists for drop-in callers
+// and is HBM-write-bound (P*D bytes out, 2*P in).
+//
+// One block per (image row, d-chunk); the R row sits in LDS behind 16 zero bytes.  A thread owns a 16-byte
+// segment of the row (its 16 L bytes stay in registers) and walks d: the R bytes x-d .. x-d+15
+// come from 5 aligned dword LDS reads and 4 v_alignbyte_b32, |L - R| is formed 2 bytes per
+// packed 16-bit lane (v_pk_sub_i16 / v_pk_max_i16), and the 16 result bytes go out as one 16-B
+// store (byte stores when the plane layout is not 16-B aligned).
+#include "bm_common.h"
+
+namespace sm {
+namespace {
+
+constexpr int kVT = 256;
+constexpr int kVPad = 16;   // zero bytes in front of the staged R row (x - d down to -15)
+
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// bytewise |a - b| of two packed u32 words
+__device__ __forceinline__ uint32_t absdiff_u8x4(uint32_t a, uint32_t b) {
+    const uint32_t ae = a & 0x00FF00FFu, ao = (a >> 8) & 0x00FF00FFu;
+    const uint32_t be = b & 0x00FF00FFu, bo = (b >> 8) & 0x00FF00FFu;
+    v2i16 de = __builtin_bit_cast(v2i16, ae) - __builtin_bit_cast(v2i16, be);
+    v2i16 dO = __builtin_bit_cast(v2i16, ao) - __builtin_bit_cast(v2i16, bo);
+    de = __builtin_elementwise_max(de, -de);
+    dO = __builtin_elementwise_max(dO, -dO);
+    return __builtin_bit_cast(uint32_t, de) | (__builtin_bit_cast(uint32_t, dO) << 8);
+}
+
+__global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                                        int W, int H, int pitch, int64_t fstride, int D,
+                                                        uint8_t* __restrict__ dif, int64_t dstride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [kVPad + W + 16]
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int dc = (D + gridDim.z - 1) / gridDim.z;               // disparities of this block
+    const int d_begin = blockIdx.z * dc, d_end = d_begin + dc < D ? d_begin + dc : D;
+    const uint8_t* lr = L + (int64_t)f * fstride + (int64_t)y * pitch;
+    const uint8_t* rr = R + (int64_t)f * fstride + (int64_t)y * pitch;
+    const int nseg = (W + 15) >> 4;
+    for (int x = threadIdx.x; x < kVPad + nseg * 16 + 4; x += kVT) {
+        const int c = x - kVPad;
+        rrow[x] = (c >= 0 && c < W) ? rr[c] : (uint8_t)0;
+    }
+    __syncthreads();
+    const int64_t P = (int64_t)W * H;
+    uint8_t* out = dif + (int64_t)f * dstride + (int64_t)y * W;
+    const bool vec = ((W & 15) == 0) && ((P & 15) == 0) && ((reinterpret_cast<uintptr_t>(dif) & 15) == 0) &&
+                     ((dstride & 15) == 0);
+    // thread -> (segment, d phase): consecutive lanes take consecutive segments of one plane row
+    const int groups = kVT / nseg > 0 ? kVT / nseg : 1;
+    const int seg = threadIdx.x % nseg, g = threadIdx.x / nseg;
+    if (g >= groups) return;
+    const int x0 = seg * 16;
+    uint32_t l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int x = x0 + 4 * q + b;
+            v |= (x < W ? (uint32_t)lr[x] : 0u) << (8 * b);
+        }
+        l[q] = v;
+    }
+#pragma unroll 2
+    for (int d = d_begin + g; d < d_end; d += groups) {
+        // R bytes at x0-d .. x0-d+15, from the padded row (index kVPad + x0 - d >= 0 while d <= x0 + 16)
+        uint32_t r[4];
+        const int start = kVPad + x0 - d;
+        if (start >= 0) {
+            const int base = start & ~3, sh = start & 3;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(rrow + base);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+            r[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            r[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            r[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            r[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        } else {
+            r[0] = r[1] = r[2] = r[3] = 0u;   // every byte of this segment has x < d: masked below
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = absdiff_u8x4(l[q], r[q]);
+        if (x0 < d + 16) {   // bytes with x < d are 0 (Device.cu:27-31 + the memset)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t keep = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) keep |= (x0 + 4 * q + b >= d ? 0xFFu : 0u) << (8 * b);
+                o[q] &= keep;
+            }
+        }
+        uint8_t* dst = out + (int64_t)d * P + x0;
+        if (vec) {
+            // streaming output (P*D bytes, larger than the MALL): nontemporal 16-B stores
+            const u32x4 v = {o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+        } else {
+            const int n = W - x0 < 16 ? W - x0 : 16;
+            for (int b = 0; b < n; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int64_t fstride, int batch,
+                            int D, uint8_t* dif, int64_t dstride, hipStream_t s) {
+    const int nseg = (W + 15) / 16;
+    if (W <= 0 || H <= 0 || D <= 0 || batch <= 0 || nseg > kVT) return hipErrorInvalidValue;
+    const size_t lds = (size_t)(kVPad + nseg * 16 + 4 + 15) & ~(size_t)15;
+    // enough blocks in flight (>= ~4 per CU of 256) to keep the stores streaming
+    int dsplit = (4096 + H * batch - 1) / (H * batch);
+    dsplit = dsplit < 1 ? 1 : (dsplit > D ? D : (dsplit > 16 ? 16 : dsplit));
+    hipLaunchKernelGGL(ad_volume_kernel, dim3(H, batch, dsplit), dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D,
+                       dif, dstride);
+    return hipGetLastError();
+}
+
+}  // namespace sm

@@ -29,6 +29,9 @@ struct sm_handle {
     // LR workspace (grown on demand): mirrored L, mirrored R, mirrored right disparity
     uint8_t* d_lr = nullptr;
     size_t lr_bytes = 0;
+    // AD volume staging of the host PreCal entry point (grown on demand)
+    uint8_t* d_vol = nullptr;
+    size_t vol_bytes = 0;
     // float maps of the host remap entry point (grown on demand)
     float* d_maps = nullptr;
     size_t maps_bytes = 0;
@@ -343,6 +346,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_rpart);
     (void)hipFree(h->d_aux);
     (void)hipFree(h->d_maps);
+    (void)hipFree(h->d_vol);
     (void)hipFree(h->d_bgr);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -512,6 +516,46 @@ SM_API int sm_remap_u8(sm_handle* h, const uint8_t* src, int width, int height, 
     SM_HIP(copy2d(h->d_left, width, src, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(sm::launch_remap(h->d_left, width, height, width, dmx, dmy, width, h->d_right, width, s));
     SM_HIP(copy2d(dst, dst_pitch, h->d_right, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
+}
+
+SM_API int sm_ad_volume_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                               int pitch, int num_disp, uint8_t* d_dif, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_left || !d_right || !d_dif || width <= 0 || height <= 0 || pitch < width || num_disp < 1 ||
+        num_disp > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "bad AD-volume arguments");
+    if (width > 4096) return fail(SM_ERR_INVALID_ARG, "width %d exceeds the AD-volume kernel's 4096 columns", width);
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_ad_volume(d_left, d_right, width, height, pitch, (int64_t)pitch * height, 1, num_disp, d_dif,
+                                (int64_t)width * height * num_disp, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_ad_volume_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+                           int num_disp, uint8_t* dif_out) {
+    int rc = check_geometry(h, width, height, pitch, 0, num_disp);
+    if (rc) return rc;
+    if (!left || !right || !dif_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
+    if (width > 4096) return fail(SM_ERR_INVALID_ARG, "width %d exceeds the AD-volume kernel's 4096 columns", width);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t need = (size_t)width * height * num_disp;
+    if (h->vol_bytes < need) {
+        if (h->d_vol) (void)hipFree(h->d_vol);
+        h->d_vol = nullptr;
+        h->vol_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_vol, need));
+        h->vol_bytes = need;
+    }
+    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(sm::launch_ad_volume(h->d_left, h->d_right, width, height, width, (int64_t)width * height, 1, num_disp,
+                                h->d_vol, (int64_t)need, s));
+    SM_HIP(hipMemcpyAsync(dif_out, h->d_vol, need, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
 }

@@ -128,6 +128,17 @@ SM_API int sm_remap_u8_device(sm_handle *h, const uint8_t *d_src, int width, int
                               const float *d_mapx, const float *d_mapy, int map_pitch,
                               uint8_t *d_dst, int dst_pitch, void *stream);
 
+/* ---- the AD cost volume itself ----
+ * dif[d][y][x] = |L(y,x) - R(y,x-d)| for x >= d, else 0, as d-major planes [num_disp][height][width]
+ * (PreCal, BlockMatching.cpp:89-109; kernalPreCal_V2 + memset, Device.cu:19-32,193-194).  The
+ * matching entry points never build it; this is for callers of the reference's PreCal.
+ * Device form: d_dif holds num_disp*width*height bytes.  Host form: synchronous, dif_out likewise.
+ * width <= 4096. */
+SM_API int sm_ad_volume_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
+                               int pitch, int num_disp, uint8_t *d_dif, void *stream);
+SM_API int sm_ad_volume_u8(sm_handle *h, const uint8_t *left, const uint8_t *right, int width, int height,
+                           int pitch, int num_disp, uint8_t *dif_out);
+
 /* ---- post-filter ----
  * (2r+1)^2 median with replicate borders, r in 1..3: ctmf (STMatching/ctmf.c:378-433) as called
  * by MeanFilter (Toolkit.cpp:33-48).  Not in place: d_src and d_dst must not overlap. */

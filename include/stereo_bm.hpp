@@ -4,8 +4,9 @@
 //   void remap_gpu(Mat &left, Mat &right, Mat &mapX1, Mat &mapY1, Mat &mapX2, Mat &mapY2,
 //                  int rows, int cols, int total, uchar *result);
 //   void cvtColor_gpu(uchar3 *src, uchar *dst, int rows, int cols);
-// on top of the C ABI in sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame, remapTest,
-// cvtColorTest) shaped caller compiles and runs unchanged apart from the include.  Host-only:
+// and BlockMatching.h's testBM / getDisp / PreCal (BlockMatching.h:8-10), on top of the C ABI in
+// sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame, remapTest, cvtColorTest) shaped caller
+// compiles and runs unchanged apart from the include.  Host-only:
 // compile it with a plain C++ compiler (it declares the host type uchar3 the reference's callers
 // cast to).
 //
@@ -191,4 +192,27 @@ inline void blockMatching_gpu(SmHostMat& h_left, SmHostMat& h_right, SmHostMat& 
 inline void remap_gpu(SmHostMat& left, SmHostMat& right, SmHostMat& mapX1, SmHostMat& mapY1, SmHostMat& mapX2,
                       SmHostMat& mapY2, int rows, int cols, int /*total*/, uchar* result) {
     sm::remap(left, right, mapX1, mapY1, mapX2, mapY2, rows, cols, result);
+}
+
+// ---- BlockMatching.h (BlockMatching.h:8-10): the reference's CPU entry points, same signatures
+//      and outputs, computed on the GPU ----
+// testBM / getDisp: the disparity map of getDisp (BlockMatching.cpp:7-87, :111-189), bit-exact.
+inline void testBM(const SmHostMat& left0, const SmHostMat& right0, SmHostMat& disparity, int SAD, int searchRange) {
+    sm::block_matching(left0, right0, disparity, SAD, searchRange);
+}
+inline void getDisp(const SmHostMat& left0, const SmHostMat& right0, uchar* disparity, int SAD, int searchRange) {
+    sm::detail::Engine& e = sm::detail::engine();
+    if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
+    if (sm_block_match_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, (int)sm::detail::row_step(left0),
+                          SAD, searchRange, SM_AGG_BOX, disparity, left0.cols) != SM_OK)
+        std::cerr << "getDisp: " << sm_last_error_string() << std::endl;
+}
+// PreCal (BlockMatching.cpp:89-109): the AD volume, searchRange d-major planes of rows*cols bytes.
+// Entries with x < d are written as 0 (the reference leaves them at the caller's memset 0).
+inline void PreCal(const SmHostMat& left0, const SmHostMat& right0, uchar* dif_, int /*SAD*/, int searchRange) {
+    sm::detail::Engine& e = sm::detail::engine();
+    if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
+    if (sm_ad_volume_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, (int)sm::detail::row_step(left0),
+                        searchRange, dif_) != SM_OK)
+        std::cerr << "PreCal: " << sm_last_error_string() << std::endl;
 }

@@ -76,3 +76,21 @@ def test_cvtcolor_test_cpp(tmp_path, gray, oracle):
     got = _read_pgm(tmp_path / "g.pgm")
     assert np.array_equal(got, oracle.bgr_to_gray(bgr))
     assert np.array_equal(got, gray["Art_/view1"])
+
+
+@pytest.mark.gpu
+def test_blockmatching_h_api_cpp(tmp_path, gray, bm_expected, oracle):
+    """testBM / getDisp / PreCal (BlockMatching.h:8-10) through stereo_bm.hpp."""
+    L, R = gray["Art/view1"], gray["Art/view5"]
+    _write_pgm(tmp_path / "l.pgm", L)
+    _write_pgm(tmp_path / "r.pgm", R)
+    env = dict(os.environ, SM_DEMO="blockMatchingApiTest", SM_LEFT=str(tmp_path / "l.pgm"),
+               SM_RIGHT=str(tmp_path / "r.pgm"), SM_SAD="3", SM_RANGE="64", SM_OUT=str(tmp_path / "a.pgm"),
+               SM_OUT2=str(tmp_path / "b.pgm"), SM_VOL=str(tmp_path / "v.u8"))
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    want = bm_expected["Art/r3/D64"]
+    assert np.array_equal(_read_pgm(tmp_path / "a.pgm"), want)
+    assert np.array_equal(_read_pgm(tmp_path / "b.pgm"), want)
+    vol = np.fromfile(tmp_path / "v.u8", np.uint8).reshape(64, *L.shape)
+    assert np.array_equal(vol, oracle.precal(L, R, 64))

@@ -323,3 +323,14 @@ def test_frame_stream_consume_callback(matcher, oracle):
     for (Ls, Rs), got in zip(batches, seen):
         for i in range(B):
             assert np.array_equal(got[i], oracle.box_disp(Ls[i], Rs[i], r, D))
+
+
+@pytest.mark.parametrize("W,H,D", [(64, 16, 8), (333, 77, 100), (1920, 1080, 128), (5, 3, 7)])
+def test_ad_volume(matcher, oracle, torch, W, H, D):
+    """PreCal / kernalPreCal_V2 (row a1) as a standalone HBM-bound kernel, bit-exact."""
+    L, R = oracle.synth_pair(W + D, W, H, max(D, 16))
+    want = oracle.precal(L, R, D)
+    assert np.array_equal(matcher.ad_volume(L, R, D), want)
+    got = matcher.ad_volume_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), D)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want)
