@@ -8,7 +8,8 @@ Three ways to spread the work over ranks:
     CPU) gives the global argmin with the reference's smallest-d tie break (strict <,
     Device.cu:57); the threshold / no-match rule is applied after the reduction;
   * row bands of ONE frame: rank k owns output rows [k*ceil(H/G), ...) and matches them from its
-    rows plus a halo (r rows for box windows, 2r for the guided filter's two nested windows);
+    rows plus a halo (r rows for box windows, 2r for the guided filter's two nested windows, +3
+    with the 7x7 median post-filter);
     a window never reaches past the halo, so each band equals the same rows of the full-frame
     result, and one all-gather of uint8 bands (H*W bytes in total) assembles the map.
 """
@@ -72,9 +73,13 @@ def band_rows(height: int, rank: int, world: int) -> Tuple[int, int]:
     return y0, min(height, y0 + n)
 
 
-def band_halo(radius: int, agg: str = "box") -> int:
-    """Input rows needed on each side of an output band."""
-    return 2 * radius if agg == "guided" else radius
+MEDIAN_RADIUS = 3   # SM_MEDIAN: 7x7 post-filter (StereoDisparity.cpp:85)
+
+
+def band_halo(radius: int, agg: str = "box", median: bool = False) -> int:
+    """Input rows needed on each side of an output band: the aggregation window (2r for the
+    guided filter's two nested windows) plus the median's 3 rows when the post-filter is on."""
+    return (2 * radius if agg == "guided" else radius) + (MEDIAN_RADIUS if median else 0)
 
 
 def band_input_rows(height: int, y0: int, y1: int, halo: int) -> Tuple[int, int]:
@@ -91,20 +96,20 @@ def gather_bands(mine, height: int, world: int, group=None):
 
 
 def band_disparity(matcher, left_t, right_t, radius: int, num_disp: int, y0: int, y1: int, agg: str = "box",
-                   lr_check: bool = False, stream=None):
+                   lr_check: bool = False, stream=None, median: bool = False):
     """Disparity rows [y0, y1) of an [H, W] device frame, matched from those rows plus the halo."""
     import torch
     H = left_t.shape[-2]
-    ys, ye = band_input_rows(H, y0, y1, band_halo(radius, agg))
+    ys, ye = band_input_rows(H, y0, y1, band_halo(radius, agg, median))
     band = matcher.match_device(left_t[ys:ye], right_t[ys:ye], radius, num_disp, agg=agg, lr_check=lr_check,
-                                stream=stream)
+                                stream=stream, median=median)
     if stream is not None:
         torch.cuda.current_stream(left_t.device).wait_stream(stream)
     return band[y0 - ys:y1 - ys]
 
 
 def match_rowband(matcher, left_t, right_t, radius: int, num_disp: int, rank: int, world: int, agg: str = "box",
-                  lr_check: bool = False, out_t=None, stream=None, group=None):
+                  lr_check: bool = False, out_t=None, stream=None, group=None, median: bool = False):
     """One [H, W] frame, row-sharded: this rank's band (with halo) -> all-gather -> full map on every rank."""
     import torch
     H, W = left_t.shape[-2:]
@@ -112,7 +117,8 @@ def match_rowband(matcher, left_t, right_t, radius: int, num_disp: int, rank: in
     y0, y1 = band_rows(H, rank, world)
     mine = torch.zeros((n, W), dtype=torch.uint8, device=left_t.device)
     if y1 > y0:
-        mine[:y1 - y0].copy_(band_disparity(matcher, left_t, right_t, radius, num_disp, y0, y1, agg, lr_check, stream))
+        mine[:y1 - y0].copy_(band_disparity(matcher, left_t, right_t, radius, num_disp, y0, y1, agg, lr_check, stream,
+                                            median))
     res = gather_bands(mine, H, world, group)
     if out_t is not None:
         out_t.copy_(res)

@@ -15,8 +15,8 @@
  * types cross this boundary.  include/stereo_bm.hpp maps the reference's Mat API
  * onto it; gpu_stereo_matching_amd/_capi.py binds it with ctypes.
  *
- * Threading: one handle per host thread.  A handle owns its device buffers,
- * pinned staging and a HIP stream; calls on one handle are serialised.
+ * Threading: one handle per host thread.  A handle owns its device buffers and a
+ * HIP stream; calls on one handle are serialised.
  */
 #ifndef SM_HIP_H
 #define SM_HIP_H

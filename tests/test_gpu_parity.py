@@ -211,20 +211,21 @@ def test_slice_keys_min_equals_full(matcher, oracle, torch, cuts):
     assert np.array_equal(d.cpu().numpy(), disp)
 
 
-@pytest.mark.parametrize("G,agg,lr", [(2, "box", False), (8, "box", False), (3, "box", True), (4, "guided", False)])
-def test_rowband_bands_equal_full_frame(matcher, torch, G, agg, lr):
+@pytest.mark.parametrize("G,agg,lr,med", [(2, "box", False, False), (8, "box", False, False), (3, "box", True, False),
+                                          (4, "guided", False, False), (5, "box", True, True), (3, "box", False, True)])
+def test_rowband_bands_equal_full_frame(matcher, torch, G, agg, lr, med):
     """The row-band partition's per-rank compute (sharding.band_disparity), run band by band on one
     GPU, reassembles the single-pass map: bit-exact for box / LR, near-ties only for guided."""
     from gpu_stereo_matching_amd import sharding
     from oracle import oracle as O
     L, R = O.synth_pair(555, 700, 203, 64)
     Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
-    full = matcher.match_device(Lt, Rt, 5, 64, agg=agg, lr_check=lr)
+    full = matcher.match_device(Lt, Rt, 5, 64, agg=agg, lr_check=lr, median=med)
     parts = []
     for k in range(G):
         y0, y1 = sharding.band_rows(203, k, G)
         if y1 > y0:
-            parts.append(sharding.band_disparity(matcher, Lt, Rt, 5, 64, y0, y1, agg, lr))
+            parts.append(sharding.band_disparity(matcher, Lt, Rt, 5, 64, y0, y1, agg, lr, median=med))
     got = torch.cat(parts)
     torch.cuda.synchronize()
     if agg == "guided":
