@@ -41,7 +41,8 @@ template <int R>
 constexpr bool kPairedScatter = (R != 3);
 template <bool RIGHT, int R>
 constexpr int kMinWavesPerEU = (RIGHT && !kWideRight<RIGHT, R>) ? 2 : 4;
-constexpr int kTileH = 32;
+constexpr int kTileH = 32;        // output rows per tile (48: 4 % slower, 3 waves/SIMD)
+constexpr int kNB = kTileH / 16;   // 16-row CS hand-off blocks per tile
 constexpr int kPairs = 4;
 constexpr int kChunk = 2 * kPairs;
 constexpr int kCols = 64;
@@ -50,7 +51,7 @@ template <int R, int DMAX, int NW = 4>
 struct Geo {
     static constexpr int TW = kCols - 2 * R;                  // output columns per tile
     static constexpr int ROWS = kTileH + 2 * R;                 // input rows per tile
-    static constexpr int HALF = kTileH / 2;                     // rows per CS hand-off
+    static constexpr int HALF = 16;                             // rows per CS hand-off
     static constexpr int NLQ = (ROWS + 3) / 4;                  // packed-L dwords per lane
     static constexpr int NQ = (((TW + 3) / 4) + 1) & ~1;        // outputs per phase-H thread (even: b64 reads)
     static constexpr int NCS2 = (NQ + 2 * R + 1) / 2;           // 8-B CS reads per phase-H thread
@@ -215,9 +216,9 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     const int hj = lane & 15;
     const int hq = lane >> 4;
     const int obase = hq * G::NQ;                  // first tile output column of this thread
-    uint32_t best[2][G::NQ];
+    uint32_t best[kNB][G::NQ];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < kNB; ++h)
 #pragma unroll
         for (int o = 0; o < G::NQ; ++o) best[h][o] = a.seed_key;
 
@@ -251,10 +252,10 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
         const bool dm = d_edge || (d + 1 >= d_hi);
         uint32_t T = 0u, Tprev[2 * R + 1];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kNB; ++h) {
             // ====== phase V (lane = CS column): input rows of this half, CS rows h*HALF.. ======
 #pragma unroll
-            for (int i = (h == 0 ? 0 : 2 * R + G::HALF); i < (h == 0 ? 2 * R + G::HALF : G::ROWS); ++i) {
+            for (int i = (h == 0 ? 0 : 2 * R + h * G::HALF); i < 2 * R + (h + 1) * G::HALF; ++i) {
                 const uint32_t w = rcol[i * G::RW];
                 const uint32_t A = __builtin_amdgcn_perm(w, lq[i >> 2], sa[i & 3]);
                 const uint32_t B = __builtin_amdgcn_perm(w, lq[i >> 2], sb[i & 3]);
@@ -348,7 +349,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     uint32_t* fold = cs;                                   // [kTileH][TW] keys
     if (wave == 0) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < kNB; ++h)
 #pragma unroll
             for (int o = 0; o < G::NQ; ++o)
                 if (obase + o < G::TW) fold[(h * G::HALF + hj) * G::TW + obase + o] = best[h][o];
@@ -356,7 +357,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     __syncthreads();
     if (wave != 0) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < kNB; ++h)
 #pragma unroll
             for (int o = 0; o < G::NQ; ++o)
                 if (obase + o < G::TW) atomicMin(&fold[(h * G::HALF + hj) * G::TW + obase + o], best[h][o]);
