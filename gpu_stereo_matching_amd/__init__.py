@@ -22,7 +22,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 from . import _capi
-from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK, SM_MEDIAN  # noqa: F401
+from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK, SM_MEDIAN, SM_STAGED  # noqa: F401
 from .synth import synth_pair  # noqa: F401
 from .gray import bgr_to_gray  # noqa: F401
 
@@ -46,9 +46,10 @@ def _as_u8_image(a, name: str) -> np.ndarray:
 
 
 def _flags(agg: str, lr_check: bool, median: bool = False) -> int:
-    if agg not in ("box", "guided"):
-        raise ValueError("agg must be 'box' or 'guided'")
-    f = SM_AGG_GUIDED if agg == "guided" else SM_AGG_BOX
+    """agg: 'box' (fused), 'box-staged' (through the AD / SAD volumes in HBM) or 'guided'."""
+    if agg not in ("box", "guided", "box-staged"):
+        raise ValueError("agg must be 'box', 'box-staged' or 'guided'")
+    f = {"box": SM_AGG_BOX, "guided": SM_AGG_GUIDED, "box-staged": SM_AGG_BOX | SM_STAGED}[agg]
     return f | (SM_LR_CHECK if lr_check else 0) | (SM_MEDIAN if median else 0)
 
 
@@ -158,6 +159,16 @@ class BlockMatcher:
         _capi.check(self._lib.sm_ad_volume_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, num_disp,
                                               out.ctypes.data))
         return out
+
+    def sad_volume_device(self, left_t, right_t, radius: int, num_disp: int, out_t=None, stream=None):
+        """u16 SAD volume [num_disp, H, W]: zero-padded (2r+1)^2 window sums of the AD planes."""
+        import torch
+        H, W = left_t.shape
+        if out_t is None:
+            out_t = torch.empty((num_disp, H, W), dtype=torch.int16, device=left_t.device)
+        _capi.check(self._lib.sm_sad_volume_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, radius,
+                                                   num_disp, out_t.data_ptr(), self._stream_ptr(stream)))
+        return out_t
 
     def ad_volume_device(self, left_t, right_t, num_disp: int, out_t=None, stream=None):
         import torch

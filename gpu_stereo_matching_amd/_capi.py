@@ -22,6 +22,7 @@ SM_AGG_BOX = 0
 SM_AGG_GUIDED = 1
 SM_LR_CHECK = 2
 SM_MEDIAN = 4
+SM_STAGED = 8
 
 SM_PARAM_GUIDED_EPS = 1
 
@@ -31,7 +32,7 @@ EXPORTED = (
     "sm_set_param_f", "sm_block_match_u8", "sm_block_match_lr_u8", "sm_last_stage_ms",
     "sm_match_device", "sm_slice_keys_device", "sm_keys_to_disp_device", "sm_stream_sync",
     "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8", "sm_median_u8_device",
-    "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8",
+    "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
 )
 
 
@@ -82,6 +83,7 @@ def load(path: str = LIB_PATH):
     L.sm_remap_u8.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i]
     L.sm_ad_volume_device.argtypes = [vp, vp, vp, i, i, i, i, vp, vp]
     L.sm_ad_volume_u8.argtypes = [vp, vp, vp, i, i, i, i, vp]
+    L.sm_sad_volume_device.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp]
     L.sm_bgr_to_gray_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
     L.sm_remap_u8_device.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i, vp]
     L.sm_block_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]

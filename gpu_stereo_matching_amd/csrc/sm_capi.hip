@@ -136,6 +136,36 @@ hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size
     return hipMemcpy2DAsync(dst, dpitch, src, spitch, row_bytes, rows, kind, s);
 }
 
+int ensure_vol(sm_handle* h, size_t bytes) {
+    if (h->vol_bytes >= bytes) return SM_OK;
+    if (h->d_vol) (void)hipFree(h->d_vol);
+    h->d_vol = nullptr;
+    h->vol_bytes = 0;
+    SM_HIP(hipMalloc(&h->d_vol, bytes));
+    h->vol_bytes = bytes;
+    return SM_OK;
+}
+
+// Staged box path, frame by frame through one AD (u8) + SAD (u16) volume workspace.
+int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch, int64_t fstride,
+               int radius, int D, bool med, uint8_t* disp, int opitch, int64_t ostride, hipStream_t s) {
+    const int64_t P = (int64_t)W * H;
+    if (W > 4096) return fail(SM_ERR_INVALID_ARG, "SM_STAGED: width %d exceeds 4096", W);
+    int rc = ensure_vol(h, (size_t)(3 * P * D) + (med ? (size_t)P : 0));
+    if (rc) return rc;
+    uint8_t* ad = h->d_vol;
+    uint16_t* sad = reinterpret_cast<uint16_t*>(h->d_vol + P * D);
+    uint8_t* raw = h->d_vol + 3 * P * D;
+    for (int f = 0; f < batch; ++f) {
+        SM_HIP(sm::launch_ad_volume(L + f * fstride, R + f * fstride, W, H, pitch, fstride, 1, D, ad, P * D, s));
+        SM_HIP(sm::launch_box_sad_volume(ad, W, H, radius, D, sad, s));
+        uint8_t* out = disp + f * ostride;
+        SM_HIP(sm::launch_volume_wta(sad, W, H, D, seed_key(radius), med ? raw : out, med ? W : opitch, s));
+        if (med) SM_HIP(sm::launch_median(raw, W, H, W, P, 1, 3, out, opitch, ostride, s));
+    }
+    return SM_OK;
+}
+
 // Core device-side pass over `batch` frames.  Workspace planes (d_lr) are dense W x H frames.
 //   left map  : matched straight into `disp`, or into a workspace plane when SM_MEDIAN filters it
 //               into `disp` afterwards (StereoDisparity.cpp:85/119);
@@ -152,6 +182,12 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     const int64_t P = (int64_t)W * H;
     const int64_t PB = P * batch;
     const bool fused_right = lr && !guided && radius <= sm::kMaxFastRadius;
+    if ((flags & SM_STAGED) != 0) {
+        if (guided || lr || radius > sm::kMaxFastRadius)
+            return fail(SM_ERR_INVALID_ARG, "SM_STAGED supports box aggregation without LR, radius <= %d",
+                        sm::kMaxFastRadius);
+        return run_staged(h, L, R, W, H, pitch, batch, fstride, radius, D, med, disp, opitch, ostride, s);
+    }
 
     // workspace: [left raw (med)] [right (lr)] [right filtered (lr && med)] [mirrored L, R (lr, not fused)]
     const int64_t n_planes = (med ? 1 : 0) + (lr ? 1 : 0) + (lr && med ? 1 : 0) + (lr && !fused_right ? 2 : 0);
@@ -544,19 +580,32 @@ SM_API int sm_ad_volume_u8(sm_handle* h, const uint8_t* left, const uint8_t* rig
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
     const size_t need = (size_t)width * height * num_disp;
-    if (h->vol_bytes < need) {
-        if (h->d_vol) (void)hipFree(h->d_vol);
-        h->d_vol = nullptr;
-        h->vol_bytes = 0;
-        SM_HIP(hipMalloc(&h->d_vol, need));
-        h->vol_bytes = need;
-    }
+    rc = ensure_vol(h, need);
+    if (rc) return rc;
     SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(sm::launch_ad_volume(h->d_left, h->d_right, width, height, width, (int64_t)width * height, 1, num_disp,
                                 h->d_vol, (int64_t)need, s));
     SM_HIP(hipMemcpyAsync(dif_out, h->d_vol, need, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
+}
+
+SM_API int sm_sad_volume_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                                int pitch, int radius, int num_disp, uint16_t* d_sad, void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!d_left || !d_right || !d_sad) return fail(SM_ERR_INVALID_ARG, "null pointer");
+    if (radius > sm::kMaxFastRadius) return fail(SM_ERR_INVALID_ARG, "SAD volume: radius %d > 7", radius);
+    if (width > 4096) return fail(SM_ERR_INVALID_ARG, "SAD volume: width %d exceeds 4096", width);
+    SM_HIP(hipSetDevice(h->device));
+    const int64_t P = (int64_t)width * height;
+    rc = ensure_vol(h, (size_t)(P * num_disp));
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    SM_HIP(sm::launch_ad_volume(d_left, d_right, width, height, pitch, (int64_t)pitch * height, 1, num_disp,
+                                h->d_vol, P * num_disp, s));
+    SM_HIP(sm::launch_box_sad_volume(h->d_vol, width, height, radius, num_disp, d_sad, s));
     return SM_OK;
 }
 

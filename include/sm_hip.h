@@ -46,10 +46,14 @@ enum {
     SM_AGG_GUIDED = 1u,     /* guided-filter aggregation of the AD volume (this build's extension) */
     SM_LR_CHECK = 2u,       /* left-right consistency (STMatching/StereoDisparity.cpp:136-147):
                                occluded pixels are written as 0 */
-    SM_MEDIAN = 4u          /* 7x7 median post-filter of the WTA map(s), STMatching's
+    SM_MEDIAN = 4u,         /* 7x7 median post-filter of the WTA map(s), STMatching's
                                MeanFilter(disp, disp, 3) = ctmf (Toolkit.cpp:33-48); with
                                SM_LR_CHECK both maps are filtered before the check, in the
                                order of StereoDisparity.cpp:119-126 */
+    SM_STAGED = 8u          /* box path through explicit HBM volumes (AD u8 -> SAD u16 -> WTA),
+                               the reference's two-kernel data flow (Device.cu:19-64); same
+                               output as the fused kernel, bandwidth-bound; not with
+                               SM_AGG_GUIDED or SM_LR_CHECK, radius <= 7 */
 };
 
 /* ---- scalar parameters (sm_set_param_f) ---- */
@@ -138,6 +142,12 @@ SM_API int sm_ad_volume_device(sm_handle *h, const uint8_t *d_left, const uint8_
                                int pitch, int num_disp, uint8_t *d_dif, void *stream);
 SM_API int sm_ad_volume_u8(sm_handle *h, const uint8_t *left, const uint8_t *right, int width, int height,
                            int pitch, int num_disp, uint8_t *dif_out);
+
+/* u16 SAD volume sad[d][y][x] = zero-padded (2r+1)^2 window sum of the AD plane d, radius <= 7
+ * (the volume kernalFindAllSAD / getAllSAD build, Device.cu:67-103 / BlockMatching.cpp:191-261,
+ * without their uint8 truncation).  d_sad holds num_disp*width*height uint16. */
+SM_API int sm_sad_volume_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
+                                int pitch, int radius, int num_disp, uint16_t *d_sad, void *stream);
 
 /* ---- post-filter ----
  * (2r+1)^2 median with replicate borders, r in 1..3: ctmf (STMatching/ctmf.c:378-433) as called

@@ -335,3 +335,35 @@ def test_ad_volume(matcher, oracle, torch, W, H, D):
     got = matcher.ad_volume_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), D)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("W,H,r,D", [(320, 256, 5, 64), (333, 77, 7, 100), (1920, 1080, 5, 128), (63, 40, 0, 8),
+                                     (463, 370, 3, 64)])
+def test_staged_equals_fused_and_oracle(matcher, oracle, torch, W, H, r, D):
+    """SM_STAGED (AD u8 -> SAD u16 -> WTA through HBM) gives the fused kernel's map, bit-exact."""
+    L, R = oracle.synth_pair(W * 7 + r, W, H, max(D, 16))
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    staged = matcher.match_device(Lt, Rt, r, D, agg="box-staged")
+    fused = matcher.match_device(Lt, Rt, r, D)
+    torch.cuda.synchronize()
+    assert torch.equal(staged, fused)
+    if W * H <= 200_000:
+        assert np.array_equal(staged.cpu().numpy(), oracle.box_disp(L, R, r, D))
+
+
+def test_sad_volume(matcher, oracle, torch):
+    L, R = oracle.synth_pair(31, 150, 60, 32)
+    sad = matcher.sad_volume_device(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), 4, 32)
+    torch.cuda.synchronize()
+    want = oracle.box_cost(L, R, 4, 32)
+    assert np.array_equal(sad.cpu().numpy().view(np.uint16).astype(np.int32), want)
+
+
+def test_staged_median_batch(matcher, oracle, torch):
+    pairs = [oracle.synth_pair(60 + b, 200, 50, 32) for b in range(3)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, 3, 32, agg="box-staged", median=True)
+    torch.cuda.synchronize()
+    for b in range(3):
+        assert np.array_equal(out[b].cpu().numpy(), oracle.median(oracle.box_disp(pairs[b][0], pairs[b][1], 3, 32), 3))
