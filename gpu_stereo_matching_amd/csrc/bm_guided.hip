@@ -14,7 +14,7 @@
 //   A region (a, b)        : (TW + 2R) x (TH + 2R) from image (x0-R, y0-R)
 //   output tile            : TW = 64 - 4R  x  TH = 32
 // Stages per d:
-//   S1V  lane = P column; waves split the A rows: prefix T += AD*(1 + 4096 L) -> packed CS rows
+//   S1V  lane = P column; waves split the A rows: prefix T += AD*(L + 2^20) -> packed CS rows
 //   S1H  thread = (A row, segment): running Sp / SIp -> a, b
 //   S2V  thread = (A column, 8-row group): running float sums of a, b over 2R+1 rows
 //   S2H  thread = (output row, segment): running sums -> N*q = sum(a) I + sum(b) -> WTA in registers
@@ -22,6 +22,8 @@
 // iteration runs {S1V(d), S2V(d-1)} | barrier | {S1H(d), S2H(d-1)} | barrier: two workgroup
 // barriers per d instead of four.  The guide statistics (SI = sum L, SII = sum L^2, N) come from
 // S1V/S1H on AD := L (R band read as 0), once per tile.
+#include <type_traits>
+
 #include "bm_common.h"
 #include "bm_guided.h"
 
@@ -53,6 +55,8 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t* p, int y, int x, int W, i
 }
 
 constexpr int kBandChunk = 64;   // disparities per staged right band
+constexpr uint32_t kPOne = 1u << 20;   // S1V multiplier L | 2^20: low 20 bits sum I*p, high 12 bits sum p
+constexpr uint32_t kPLow = kPOne - 1;
 
 template <int R>
 struct GeoF {
@@ -63,6 +67,8 @@ struct GeoF {
     static constexpr int PH = TH + 4 * R;
     static constexpr int RPW = (AH + 3) / 4;                 // A rows per wave in S1V
     static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
+    static constexpr int AHP = 4 * RPW;                      // cs rows incl. the last wave's pad rows
+    static constexpr int PHP = 4 * RPW + 2 * R;              // staged P rows incl. pad rows (>= PH)
     static constexpr int NSEG1 = kT / AH;                    // S1H segments per A row
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
@@ -70,15 +76,16 @@ struct GeoF {
     // strides kept minimal so that r <= 5 fits 3 workgroups per CU (<= 52 KB): an odd CS stride
     // spreads the S1H rows over the banks (padding mm / a/b rows for banks measured slower).
     // S2H threads whose last outputs fall past TW read beyond their mm row (the next row, or abp
-    // after the last one) into values that only reach those discarded outputs.
+    // after the last one) into values that only reach those discarded outputs.  S1H writes every
+    // one of its NSEG1*SW1 columns (those past AW are never read), so a/b rows are that wide.
     static constexpr int CSS = CSS0 + 1;                     // u32 per CS row
     static constexpr int MS = AW;                            // float2 per mm row
-    static constexpr int ABS = AW;                           // float2 per a/b row
+    static constexpr int ABS = NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW;   // float2 per a/b row
     static constexpr int RBW = 64 + kBandChunk;              // right band bytes per P row (one d-chunk)
-    static constexpr int CS_BYTES = ((AH * CSS * 4 > PH * 64 ? AH * CSS * 4 : PH * 64) + 15) & ~15;  // lt aliases cs
+    static constexpr int CS_BYTES = ((AHP * CSS * 4 > PHP * 64 ? AHP * CSS * 4 : PHP * 64) + 15) & ~15;  // lt aliases cs
     static constexpr int MM_BYTES = TH * MS * 8;
     static constexpr int AB_BYTES = AH * ABS * 8;
-    static constexpr int RB_BYTES = (PH * RBW + 15) & ~15;
+    static constexpr int RB_BYTES = (PHP * RBW + 15) & ~15;
     static constexpr int LDS = CS_BYTES + MM_BYTES + AB_BYTES + RB_BYTES;
 };
 
@@ -93,13 +100,14 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     int tiles) {
     using G = GeoF<R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AH][CSS] packed sums
-    uint8_t* lt = smem;                                                                 // [PH][64] (aliases cs)
+    uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
+    uint8_t* lt = smem;                                                                 // [PHP][64] (aliases cs)
     float2* mm = reinterpret_cast<float2*>(smem + G::CS_BYTES);                        // [TH][MS]
     float2* abp = reinterpret_cast<float2*>(smem + G::CS_BYTES + G::MM_BYTES);         // [AH][ABS]
-    uint8_t* rb = smem + G::CS_BYTES + G::MM_BYTES + G::AB_BYTES;                      // [PH][RBW]
+    uint8_t* rb = smem + G::CS_BYTES + G::MM_BYTES + G::AB_BYTES;                      // [PHP][RBW]
 
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: S1V's row range
     const int tile_id = xcd_tile(blockIdx.x, gridDim.x);
     const int frame = tile_id / tiles;
     const int t = tile_id - frame * tiles;
@@ -113,25 +121,28 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     //      disparity d (in chunk k) reads rb[i][c + 64 - (d & 63)] ----
     auto stage_band = [&](int k) {
         const int rbase = px0 - kBandChunk * k - kBandChunk;
-        for (int e = tid; e < G::PH * (G::RBW / 4); e += kT) {
+        for (int e = tid; e < G::PHP * (G::RBW / 4); e += kT) {
             const int i = e / (G::RBW / 4), j = e - (e / (G::RBW / 4)) * (G::RBW / 4);
             *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = ld4(Rf, py0 + i, rbase + 4 * j, W, H, pitch);
         }
     };
     stage_band(0);
-    for (int e = tid; e < G::PH * 16; e += kT) {
+    for (int e = tid; e < G::PHP * 16; e += kT) {
         const int i = e >> 4, j = e & 15;
         *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = ld4(L, py0 + i, px0 + 4 * j, W, H, pitch);
     }
     __syncthreads();
-    // S1V state: this wave walks P rows [a0, a0 + NV); lane = P column c
+    // S1V state: this wave walks P rows [a0, a0 + NV) (rows past PH are pad rows that only reach
+    // the pad rows of cs); lane = P column c
     const int a0 = wave * G::RPW;
     const int c = lane;
     const int xc = px0 + c;
     const bool col_in = xc >= 0 && xc < W;
-    uint32_t lzm[G::NV];   // (L << 12) | 1: the S1V multiplier; L itself is lzm >> 12
+    // m = L | 2^20: T += AD * m accumulates sum(I*p) in the low 20 bits (<= 15 * 255^2 < 2^20) and
+    // sum(p) above them; v_sad_u8(m, R, -16) = |L - R| + |0x10 - 0| - 16 = AD exactly
+    uint32_t mul[G::NV];
 #pragma unroll
-    for (int k = 0; k < G::NV; ++k) lzm[k] = (((a0 + k < G::PH) ? (uint32_t)lt[(a0 + k) * 64 + c] : 0u) << 12) | 1u;
+    for (int k = 0; k < G::NV; ++k) mul[k] = (uint32_t)lt[(a0 + k) * 64 + c] | kPOne;
     __syncthreads();   // lt (aliased with cs) is consumed
 
     // S1H ownership: A row h1i, segment h1s (threads >= AH*NSEG1 idle in S1H)
@@ -149,10 +160,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     // per-A-pixel constants (filled by the stats pass) and per-output WTA state.
     // WTA runs on N*q = sum(a)*I + sum(b): N (output window count) is a positive per-pixel
     // constant, so the argmin is that of q; the Device.cu:37 seed 50 becomes 50*N (exact in fp32).
-    uint32_t nN[G::SW1], nSI[G::SW1];
-    float invden[G::SW1], invN[G::SW1];
+    // A pixels outside the image get invden = invN = 0, so their a and b come out 0.
+    uint32_t nN[G::SW1];
+    uint32_t nSI[G::SW1];
+    float fSI[G::SW1], invden[G::SW1], invN[G::SW1];
     float oI[G::SW2], bq[G::SW2];
-    int bdd[G::SW2];
+    int bdd[G::SW2], dlim[G::SW2];
 #pragma unroll
     for (int o = 0; o < G::SW2; ++o) {
         const int x = x0 + h2s * G::SW2 + o;
@@ -160,86 +173,111 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         oI[o] = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
+        dlim[o] = valid_mode == 0 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
     }
 
-    // ================= S1V: d < 0 is the guide-statistics pass (AD := L) =================
-    auto s1v = [&](int d) {
-        const bool m = d < 0 ? true : (col_in && xc >= d);
-        const uint8_t* rc = rb + (c + kBandChunk - (d < 0 ? 0 : (d & (kBandChunk - 1))));
+    // ================= S1V =================
+    // STATS: the guide statistics pass, AD := L (the R band read as 0)
+    auto s1v = [&](int d, auto stats) {
+        constexpr bool STATS = decltype(stats)::value;
+        const bool m = STATS || (col_in && xc >= d);
+        const uint8_t* rc = rb + (c + kBandChunk - (d & (kBandChunk - 1)));
+        uint32_t rv[G::NV];
+#pragma unroll
+        for (int k = 0; k < G::NV; ++k) rv[k] = STATS ? 0u : (uint32_t)rc[(a0 + k) * G::RBW];
         uint32_t T = 0u, Tp[2 * R + 1];
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) {
-            const int i = a0 + k;                                   // P row
-            const uint32_t rv = (d < 0 || i >= G::PH) ? 0u : (uint32_t)rc[i * G::RBW];
-            uint32_t ad = __builtin_amdgcn_sad_u8(lzm[k] >> 12, rv, 0u);
-            ad = m ? ad : 0u;
-            T = __umul24(ad, lzm[k]) + T;
+            const uint32_t ad = __builtin_amdgcn_sad_u8(mul[k], rv[k], 0xFFFFFFF0u);
+            T = __umul24(ad, mul[k]) + T;
             if (k >= 2 * R) {
                 const uint32_t old = (k == 2 * R) ? 0u : Tp[(k - 2 * R - 1) % (2 * R + 1)];
-                const int j = i - 2 * R;                            // A row
-                if (j < a0 + G::RPW && j < G::AH) cs[j * G::CSS + c] = T - old;
+                cs[(a0 + k - 2 * R) * G::CSS + c] = m ? T - old : 0u;
             }
             Tp[k % (2 * R + 1)] = T;
         }
     };
     // ================= S1H =================
-    auto s1h = [&](int d) {
+    auto s1h_stats = [&]() {
         if (!h1_on) return;
         const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
         uint32_t sp = 0, sip = 0;
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
             const uint32_t v = row[k];
-            sp += v & 0xFFFu;
-            sip += v >> 12;
+            sp += v >> 20;
+            sip += v & kPLow;
         }
 #pragma unroll
         for (int o = 0; o < G::SW1; ++o) {
             const uint32_t vin = row[o + 2 * R];
-            sp += vin & 0xFFFu;
-            sip += vin >> 12;
+            sp += vin >> 20;
+            sip += vin & kPLow;
+            // guide statistics: sp = SI, sip = SII
             const int j = h1s * G::SW1 + o;                         // A column
             const int x = x0 - R + j;
             const bool inimg = h1y >= 0 && h1y < H && x >= 0 && x < W && j < G::AW;
-            if (d < 0) {
-                // guide statistics: sp = SI, sip = SII
-                const uint32_t N = inimg ? (uint32_t)(win_count(x, R, W) * win_count(h1y, R, H)) : 1u;
-                const int32_t nvar = (int32_t)(N * sip - sp * sp);
-                nN[o] = N;
-                nSI[o] = sp;
-                invden[o] = 1.0f / ((float)nvar + eps * (float)N * (float)N);
-                invN[o] = inimg ? 1.0f / (float)N : 0.f;
-            } else if (j < G::AW) {
-                const int32_t num = (int32_t)(nN[o] * sip - nSI[o] * sp);
-                const float a = (float)num * invden[o];
-                const float b = ((float)sp - a * (float)nSI[o]) * invN[o];
-                abp[h1i * G::ABS + j] = inimg ? make_float2(a, b) : make_float2(0.f, 0.f);
-            }
+            const uint32_t N = inimg ? (uint32_t)(win_count(x, R, W) * win_count(h1y, R, H)) : 1u;
+            const int32_t nvar = (int32_t)(N * sip - sp * sp);
+            nN[o] = N;
+            nSI[o] = sp;
+            fSI[o] = (float)sp;
+            invden[o] = inimg ? 1.0f / ((float)nvar + eps * (float)N * (float)N) : 0.f;
+            invN[o] = inimg ? 1.0f / (float)N : 0.f;
             const uint32_t vout = row[o];
-            sp -= vout & 0xFFFu;
-            sip -= vout >> 12;
+            sp -= vout >> 20;
+            sip -= vout & kPLow;
+        }
+    };
+    auto s1h = [&]() {
+        if (!h1_on) return;
+        const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
+        float2* dst = abp + h1i * G::ABS + h1s * G::SW1;
+        // the whole segment is loaded before the first a/b store (the compiler cannot tell abp
+        // from cs, so interleaved loads would each wait for the stores before them)
+        uint32_t v[G::SW1 + 2 * R];
+#pragma unroll
+        for (int k = 0; k < G::SW1 + 2 * R; ++k) v[k] = row[k];
+        uint32_t sp = 0, sip = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * R; ++k) {
+            sp += v[k] >> 20;
+            sip += v[k] & kPLow;
+        }
+#pragma unroll
+        for (int o = 0; o < G::SW1; ++o) {
+            sp += v[o + 2 * R] >> 20;
+            sip += v[o + 2 * R] & kPLow;
+            // N*SIp - SI*Sp = N^2 cov(I, p), |.| < 2^30: the products' low words (factors < 2^24)
+            // subtracted mod 2^32 give it exactly
+            const int32_t num = (int32_t)(__umul24(nN[o], sip) - __umul24(nSI[o], sp));
+            const float a = (float)num * invden[o];
+            const float b = __builtin_fmaf(-a, fSI[o], (float)sp) * invN[o];
+            dst[o] = make_float2(a, b);
+            sp -= v[o] >> 20;
+            sip -= v[o] & kPLow;
         }
     };
     // ================= S2V =================
     auto s2v = [&]() {
         if (!v2_on) return;
         const float2* col = abp + v2j;
+        float2 v[8 + 2 * R];   // loaded before the mm stores, as in S1H
+#pragma unroll
+        for (int k = 0; k < 8 + 2 * R; ++k) v[k] = col[(8 * v2g + k) * G::ABS];
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
-            const float2 v = col[(8 * v2g + k) * G::ABS];
-            sa += v.x;
-            sb += v.y;
+            sa += v[k].x;
+            sb += v[k].y;
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const float2 vin = col[(8 * v2g + r + 2 * R) * G::ABS];
-            sa += vin.x;
-            sb += vin.y;
+            sa += v[r + 2 * R].x;
+            sb += v[r + 2 * R].y;
             mm[(8 * v2g + r) * G::MS + v2j] = make_float2(sa, sb);
-            const float2 vout = col[(8 * v2g + r) * G::ABS];
-            sa -= vout.x;
-            sb -= vout.y;
+            sa -= v[r].x;
+            sb -= v[r].y;
         }
     };
     // ================= S2H + WTA =================
@@ -258,31 +296,28 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
             sa += vin.x;
             sb += vin.y;
             const float q = sa * oI[o] + sb;
-            const int x = x0 + h2s * G::SW2 + o;
-            const int lim = valid_mode == 0 ? (W - x) : x;
-            if (d <= lim && q < bq[o]) {
-                bq[o] = q;
-                bdd[o] = d;
-            }
+            const bool take = d <= dlim[o] && q < bq[o];
+            bq[o] = take ? q : bq[o];
+            bdd[o] = take ? d : bdd[o];
             const float2 vout = row[o];
             sa -= vout.x;
             sb -= vout.y;
         }
     };
 
-    s1v(-1);
+    s1v(0, std::true_type{});
     __syncthreads();
-    s1h(-1);
+    s1h_stats();
     __syncthreads();
     // buffers: cs (S1V -> S1H), abp (S1H -> S2V), mm (S2V -> S2H); each producer of iteration d+1
     // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
     // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
     for (int d = 0; d <= D; ++d) {
-        if (d < D) s1v(d);
+        if (d < D) s1v(d, std::false_type{});
         if (d > 0) s2v();
         __syncthreads();
         if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
-        if (d < D) s1h(d);
+        if (d < D) s1h();
         if (d > 0) s2h(d - 1);
         __syncthreads();
     }
