@@ -54,7 +54,9 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t* p, int y, int x, int W, i
     return v;
 }
 
-constexpr int kBandChunk = 64;   // disparities per staged right band
+// disparities per staged right band: 32 keeps LDS <= 52.3 KB at r = 5 with the bank-spread CS stride
+// (3 workgroups/CU; measured occupancy drops to 2 at 54 KB)
+constexpr int kBandChunk = 32;
 constexpr uint32_t kPOne = 1u << 20;   // S1V multiplier L | 2^20: low 20 bits sum I*p, high 12 bits sum p
 constexpr uint32_t kPLow = kPOne - 1;
 
@@ -78,7 +80,16 @@ struct GeoF {
     // S2H threads whose last outputs fall past TW read beyond their mm row (the next row, or abp
     // after the last one) into values that only reach those discarded outputs.  S1H writes every
     // one of its NSEG1*SW1 columns (those past AW are never read), so a/b rows are that wide.
-    static constexpr int CSS = CSS0 + 1;                     // u32 per CS row
+    // S1H thread tid reads CS dword h1i*CSS + h1s*SW1 + k (h1i = tid / NSEG1, h1s = tid % NSEG1):
+    // with SW1 odd and CSS == NSEG1*SW1 (mod 32) that is SW1*tid + k (mod 32), a distinct bank for
+    // each lane of a 32-lane group (the odd CS stride left 2-way conflicts, 25 % of LDS cycles)
+    static constexpr int CSS_B = CSS0 + ((NSEG1 * SW1 - CSS0) % 32 + 32) % 32;
+    static constexpr int CSS_OLD = CSS0 + 1;
+    static constexpr int lds_for(int css) {
+        return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + TH * AW * 8 +
+               AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
+    }
+    static constexpr int CSS = (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : 53248)) ? CSS_B : CSS_OLD;
     static constexpr int MS = AW;                            // float2 per mm row
     static constexpr int ABS = NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW;   // float2 per a/b row
     static constexpr int RBW = 64 + kBandChunk;              // right band bytes per P row (one d-chunk)
@@ -149,9 +160,17 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     const bool h1_on = tid < G::AH * G::NSEG1;
     const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
     const int h1y = y0 - R + h1i;
-    // S2V ownership: A column v2j, output rows [8*v2g, 8*v2g + 8)
-    const bool v2_on = tid < 4 * G::AW;
-    const int v2g = v2_on ? tid / G::AW : 0, v2j = v2_on ? tid % G::AW : 0;
+    // S2V ownership: A column v2j = lane, output rows [8*v2g, 8*v2g + 8) with v2g = wave (one row
+    // group per wave: its lanes read one contiguous a/b row span, no bank conflicts at a wrap)
+    const bool v2_on = lane < G::AW;
+    const int v2g = wave, v2j = v2_on ? lane : 0;
+    const float2* v2col[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        uint32_t off = (uint32_t)(((8 * v2g + k) * G::ABS + v2j) * 8);
+        asm volatile("" : "+v"(off));
+        v2col[k] = reinterpret_cast<const float2*>(reinterpret_cast<const uint8_t*>(abp) + off);
+    }
     // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2); rows run across lanes
     // (measured 2 % faster than segments across lanes)
     const int h2r = tid & 31, h2s = tid >> 5;
@@ -178,9 +197,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
 
     // ================= S1V =================
     // STATS: the guide statistics pass, AD := L (the R band read as 0)
-    auto s1v = [&](int d, auto stats) {
+    // NOMASK: every P column of the tile is inside the image and >= every d (tile-uniform)
+    auto s1v = [&](int d, auto stats, auto nomask) {
         constexpr bool STATS = decltype(stats)::value;
-        const bool m = STATS || (col_in && xc >= d);
+        constexpr bool NOMASK = decltype(nomask)::value;
+        const bool m = STATS || NOMASK || (col_in && xc >= d);
         const uint8_t* rc = rb + (c + kBandChunk - (d & (kBandChunk - 1)));
         uint32_t rv[G::NV];
 #pragma unroll
@@ -220,7 +241,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
             const uint32_t N = inimg ? (uint32_t)(win_count(x, R, W) * win_count(h1y, R, H)) : 1u;
             const int32_t nvar = (int32_t)(N * sip - sp * sp);
             nN[o] = N;
-            nSI[o] = sp;
+            nSI[o] = 0u - sp;   // -SI, for the signed 24-bit products in S1H
             fSI[o] = (float)sp;
             invden[o] = inimg ? 1.0f / ((float)nvar + eps * (float)N * (float)N) : 0.f;
             invN[o] = inimg ? 1.0f / (float)N : 0.f;
@@ -248,9 +269,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         for (int o = 0; o < G::SW1; ++o) {
             sp += v[o + 2 * R] >> 20;
             sip += v[o + 2 * R] & kPLow;
-            // N*SIp - SI*Sp = N^2 cov(I, p), |.| < 2^30: the products' low words (factors < 2^24)
-            // subtracted mod 2^32 give it exactly
-            const int32_t num = (int32_t)(__umul24(nN[o], sip) - __umul24(nSI[o], sp));
+            // N*SIp - SI*Sp = N^2 cov(I, p), |.| < 2^30, exactly: every factor fits a signed 24-bit
+            // operand (SIp <= 121 * 255^2 < 2^23), so v_mul_i32_i24 + v_mad_i32_i24 (written out: the
+            // compiler otherwise turns one product into a quarter-rate v_mul_lo_u32)
+            int32_t num;
+            asm("v_mul_i32_i24 %0, %1, %2" : "=v"(num) : "v"(nSI[o]), "v"(sp));
+            asm("v_mad_i32_i24 %0, %1, %2, %0" : "+v"(num) : "v"(nN[o]), "v"(sip));
             const float a = (float)num * invden[o];
             const float b = __builtin_fmaf(-a, fSI[o], (float)sp) * invN[o];
             dst[o] = make_float2(a, b);
@@ -261,10 +285,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     // ================= S2V =================
     auto s2v = [&]() {
         if (!v2_on) return;
-        const float2* col = abp + v2j;
+        // one ds_read_b64 per row (2 LDS cycles) instead of a merged ds_read2_b64 (8 cycles for the
+        // same two rows, MI355X_MICROARCH.md LDS table): rows k and k + 5 share a base whose value the
+        // compiler cannot relate to the others, and 5 rows (2160 B) exceed ds_read2's offset range
         float2 v[8 + 2 * R];   // loaded before the mm stores, as in S1H
 #pragma unroll
-        for (int k = 0; k < 8 + 2 * R; ++k) v[k] = col[(8 * v2g + k) * G::ABS];
+        for (int k = 0; k < 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
@@ -281,7 +307,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         }
     };
     // ================= S2H + WTA =================
-    auto s2h = [&](int d) {
+    // LIM: some output of the tile can have d > its dlim (tile-uniform; interior tiles skip the test)
+    auto s2h = [&](int d, auto lim) {
+        constexpr bool LIM = decltype(lim)::value;
         const float2* row = mm + h2r * G::MS + h2s * G::SW2;
         float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -296,7 +324,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
             sa += vin.x;
             sb += vin.y;
             const float q = sa * oI[o] + sb;
-            const bool take = d <= dlim[o] && q < bq[o];
+            const bool take = (!LIM || d <= dlim[o]) && q < bq[o];
             bq[o] = take ? q : bq[o];
             bdd[o] = take ? d : bdd[o];
             const float2 vout = row[o];
@@ -305,7 +333,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         }
     };
 
-    s1v(0, std::true_type{});
+    s1v(0, std::true_type{}, std::false_type{});
+    const bool s1_nomask = px0 >= D - 1 && px0 >= 0 && px0 + 63 < W;
+    const bool s2_lim = valid_mode == 0 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
     __syncthreads();
     s1h_stats();
     __syncthreads();
@@ -313,12 +343,18 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
     // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
     for (int d = 0; d <= D; ++d) {
-        if (d < D) s1v(d, std::false_type{});
+        if (d < D) {
+            if (s1_nomask) s1v(d, std::false_type{}, std::true_type{});
+            else s1v(d, std::false_type{}, std::false_type{});
+        }
         if (d > 0) s2v();
         __syncthreads();
         if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
         if (d < D) s1h();
-        if (d > 0) s2h(d - 1);
+        if (d > 0) {
+            if (s2_lim) s2h(d - 1, std::true_type{});
+            else s2h(d - 1, std::false_type{});
+        }
         __syncthreads();
     }
     uint8_t* Df = disp + (int64_t)frame * ostride;

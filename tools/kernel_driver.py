@@ -14,7 +14,11 @@ ap.add_argument("--D", type=int, default=128)
 ap.add_argument("--r", type=int, default=5)
 ap.add_argument("--agg", default="box")
 ap.add_argument("--lr", action="store_true")
+ap.add_argument("--lib", default=None, help="libsm_hip.so build to load (A/B profiling)")
 a = ap.parse_args()
+if a.lib:
+    import gpu_stereo_matching_amd._capi as C
+    C.load(a.lib)
 m = sm.BlockMatcher(0, a.W, a.H, 256)
 pairs = [sm.synth_pair(1234 + i, a.W, a.H, a.D) for i in range(a.batch)]
 Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
