@@ -160,6 +160,14 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     const bool h1_on = tid < G::AH * G::NSEG1;
     const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
     const int h1y = y0 - R + h1i;
+    // S1H's a/b row segment, its LDS offset pinned in a VGPR: the compiler otherwise re-adds the
+    // region offset before every store (ds_write2 offsets are 8-bit)
+    float2* h1dst;
+    {
+        uint32_t off = (uint32_t)(reinterpret_cast<uint8_t*>(abp + h1i * G::ABS + h1s * G::SW1) - smem);
+        asm volatile("" : "+v"(off));
+        h1dst = reinterpret_cast<float2*>(smem + off);
+    }
     // S2V ownership: A column v2j = lane, output rows [8*v2g, 8*v2g + 8) with v2g = wave (one row
     // group per wave: its lanes read one contiguous a/b row span, no bank conflicts at a wrap)
     const bool v2_on = lane < G::AW;
@@ -253,7 +261,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     auto s1h = [&]() {
         if (!h1_on) return;
         const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
-        float2* dst = abp + h1i * G::ABS + h1s * G::SW1;
+        float2* dst = h1dst;
         // the whole segment is loaded before the first a/b store (the compiler cannot tell abp
         // from cs, so interleaved loads would each wait for the stores before them)
         uint32_t v[G::SW1 + 2 * R];
