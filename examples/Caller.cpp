@@ -56,35 +56,38 @@ void singleFrame() {
     write_pgm(env_or("SM_OUT", "disp.pgm"), disp);                    // imshow("disp", disp) in the reference
 }
 
-// remapTest (Caller.cpp:27-74): rectify a pair with remap_gpu.  Without OpenCV/YAML in this
-// image the CV_32FC1 maps come from raw float files (SM_MAPX / SM_MAPY, rows*cols floats each)
-// instead of LoadDataBatch + Rectify; the left result is written as PGM instead of imshow.
-static bool read_f32(const std::string& path, sm::Mat& m, int rows, int cols) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
-    m.create(rows, cols, CV_32FC1);
-    f.read(reinterpret_cast<char*>(m.data), (std::streamsize)(m.step * rows));
-    return (bool)f;
-}
-
+// remapTest (Caller.cpp:27-74): the reference's chain on the gray, already-resized pair —
+// LoadDataBatch (the YAML calibration, SM_CALIB) -> Rectify (stereoRectify + the CV_32FC1 maps on the
+// GPU) -> remap_gpu.  Both rectified views are written as PGM (SM_OUT, SM_OUT2) instead of imshow,
+// and the four maps as raw float32 planes (SM_MAPS, optional).
 void remapTest() {
-    sm::Mat left, right, mapX1, mapY1;
-    if (!read_pgm(env_or("SM_LEFT", "view1_.pgm"), left) || !read_pgm(env_or("SM_RIGHT", "view5_.pgm"), right)) {
+    sm::Mat left, right, mapX1, mapY1, mapX2, mapY2;
+    sm::Mat camMat1, camMat2, distCoe1, distCoe2, R, T;
+    if (!read_pgm(env_or("SM_LEFT", "left_320x200.pgm"), left) ||
+        !read_pgm(env_or("SM_RIGHT", "right_320x200.pgm"), right)) {
         std::cerr << "cannot read the pair" << std::endl;
         std::exit(2);
     }
     const int rows = left.rows, cols = left.cols, total = rows * cols;
-    if (!read_f32(env_or("SM_MAPX", "mapx.f32"), mapX1, rows, cols) ||
-        !read_f32(env_or("SM_MAPY", "mapy.f32"), mapY1, rows, cols)) {
-        std::cerr << "cannot read the maps" << std::endl;
+    if (!sm::LoadDataBatch(env_or("SM_CALIB", "Calib_Data_OpenCV.yml"), camMat1, camMat2, distCoe1, distCoe2, R, T))
         std::exit(2);
-    }
-    sm::Mat result(rows, cols);
+    if (sm::Rectify(camMat1, camMat2, distCoe1, distCoe2, R, T, sm::Size(cols, rows), mapX1, mapY1, mapX2, mapY2) !=
+        SM_OK)
+        std::exit(3);
+    sm::Mat result(rows, cols), result2(rows, cols);
     auto t0 = std::chrono::steady_clock::now();
-    remap_gpu(left, right, mapX1, mapY1, mapX1, mapY1, rows, cols, total, result.data);
+    remap_gpu(left, right, mapX1, mapY1, mapX2, mapY2, rows, cols, total, result.data);
     auto t1 = std::chrono::steady_clock::now();
     std::cout << "GPU Remap : " << std::chrono::duration<double, std::milli>(t1 - t0).count() << std::endl;
-    write_pgm(env_or("SM_OUT", "remap.pgm"), result);
+    sm::remap(left, right, mapX1, mapY1, mapX2, mapY2, rows, cols, result.data, result2.data);
+    write_pgm(env_or("SM_OUT", "remap_left.pgm"), result);
+    write_pgm(env_or("SM_OUT2", "remap_right.pgm"), result2);
+    const std::string maps = env_or("SM_MAPS", "");
+    if (!maps.empty()) {
+        std::ofstream f(maps, std::ios::binary);
+        for (const sm::Mat* m : {&mapX1, &mapY1, &mapX2, &mapY2})
+            f.write(reinterpret_cast<const char*>(m->data), (std::streamsize)(m->step * rows));
+    }
 }
 
 // cvtColorTest (Caller.cpp:76-113): BGR -> gray with cvtColor_gpu on a binary PPM (P6, RGB order on

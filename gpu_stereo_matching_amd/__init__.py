@@ -199,6 +199,41 @@ class BlockMatcher:
                                                  mapy_t.data_ptr(), W, out_t.data_ptr(), W, self._stream_ptr(stream)))
         return out_t
 
+    @staticmethod
+    def _map_args(K, dist, R, P):
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        d = np.ascontiguousarray(dist if dist is not None else [], np.float64).ravel()
+        R = np.ascontiguousarray(R, np.float64).reshape(9)
+        P = np.ascontiguousarray(P, np.float64).reshape(12)
+        return K, d, R, P
+
+    def init_rectify_map(self, K, dist, R, P, width: int, height: int):
+        """initUndistortRectifyMap(K, dist, R, P, (width, height), CV_32FC1) computed on the GPU
+        (Utility.cpp:232-233): float32 (mapx, mapy) host arrays [height, width]."""
+        K, d, R, P = self._map_args(K, dist, R, P)
+        mx = np.empty((height, width), np.float32)
+        my = np.empty((height, width), np.float32)
+        vp = ctypes.c_void_p
+        _capi.check(self._lib.sm_init_rectify_map(self._h, K.ctypes.data_as(vp), d.ctypes.data_as(vp) if d.size else None,
+                                                  d.size, R.ctypes.data_as(vp), P.ctypes.data_as(vp), width, height,
+                                                  mx.ctypes.data, my.ctypes.data, width))
+        return mx, my
+
+    def init_rectify_map_device(self, K, dist, R, P, width: int, height: int, mapx_t=None, mapy_t=None, stream=None):
+        """Device form of :meth:`init_rectify_map`: float32 [height, width] CUDA tensors."""
+        import torch
+        K, d, R, P = self._map_args(K, dist, R, P)
+        if mapx_t is None:
+            mapx_t = torch.empty((height, width), dtype=torch.float32, device=f"cuda:{self.device}")
+        if mapy_t is None:
+            mapy_t = torch.empty((height, width), dtype=torch.float32, device=f"cuda:{self.device}")
+        vp = ctypes.c_void_p
+        _capi.check(self._lib.sm_init_rectify_map_device(
+            self._h, K.ctypes.data_as(vp), d.ctypes.data_as(vp) if d.size else None, d.size, R.ctypes.data_as(vp),
+            P.ctypes.data_as(vp), width, height, mapx_t.data_ptr(), mapy_t.data_ptr(), mapx_t.stride(0),
+            self._stream_ptr(stream)))
+        return mapx_t, mapy_t
+
     def median_device(self, src_t, radius: int = 3, out_t=None, stream=None):
         """(2r+1)^2 median, replicate borders (ctmf, STMatching/ctmf.c), r in 1..3; src [H, W] uint8."""
         import torch

@@ -33,6 +33,7 @@ EXPORTED = (
     "sm_match_device", "sm_slice_keys_device", "sm_keys_to_disp_device", "sm_stream_sync",
     "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8", "sm_median_u8_device",
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
+    "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
 )
 
 
@@ -87,6 +88,9 @@ def load(path: str = LIB_PATH):
     L.sm_bgr_to_gray_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
     L.sm_remap_u8_device.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i, vp]
     L.sm_block_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
+    L.sm_stereo_rectify.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp]
+    L.sm_init_rectify_map_device.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i, vp]
+    L.sm_init_rectify_map.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

@@ -71,4 +71,12 @@ hipError_t launch_bgr_to_gray(const uint8_t* src, int W, int H, int pitch, int c
 hipError_t launch_remap(const uint8_t* src, int W, int H, int pitch, const float* mapx, const float* mapy, int mpitch,
                         uint8_t* dst, int dpitch, hipStream_t s);
 
+// rectification (bm_rectify.hip): OpenCV 2.4 stereoRectify (CV_CALIB_ZERO_DISPARITY, alpha = -1) on the
+// host, and initUndistortRectifyMap (CV_32FC1) on the GPU.  r_len: 9 (3x3 matrix) or 3 (rotation vector).
+bool stereo_rectify(const double* K1, const double* dist1, int ndist1, const double* K2, const double* dist2,
+                    int ndist2, int width, int height, const double* R, int r_len, const double* T, double* R1,
+                    double* R2, double* P1, double* P2, double* Q);
+hipError_t launch_rectify_map(const double* K, const double* dist, int ndist, const double* R, const double* P,
+                              int W, int H, float* mapx, float* mapy, int map_pitch, hipStream_t s);
+
 }  // namespace sm

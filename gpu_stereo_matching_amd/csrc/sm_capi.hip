@@ -556,6 +556,72 @@ SM_API int sm_remap_u8(sm_handle* h, const uint8_t* src, int width, int height, 
     return SM_OK;
 }
 
+SM_API int sm_stereo_rectify(const double* K1, const double* dist1, int ndist1, const double* K2, const double* dist2,
+                             int ndist2, int width, int height, const double* R, int r_len, const double* T, double* R1,
+                             double* R2, double* P1, double* P2, double* Q) {
+    if (!K1 || !K2 || !R || !T || !R1 || !R2 || !P1 || !P2 || !Q || width <= 0 || height <= 0)
+        return fail(SM_ERR_INVALID_ARG, "bad stereo_rectify arguments");
+    auto ndist_ok = [](int n, const double* d) { return (n == 0 || n == 4 || n == 5 || n == 8) && (n == 0 || d); };
+    if (!ndist_ok(ndist1, dist1) || !ndist_ok(ndist2, dist2))
+        return fail(SM_ERR_INVALID_ARG, "distortion vectors hold 0, 4, 5 or 8 coefficients");
+    if (r_len != 9 && r_len != 3) return fail(SM_ERR_INVALID_ARG, "R is a 3x3 matrix (9) or a rotation vector (3)");
+    if (!sm::stereo_rectify(K1, dist1, ndist1, K2, dist2, ndist2, width, height, R, r_len, T, R1, R2, P1, P2, Q))
+        return fail(SM_ERR_INVALID_ARG, "singular rotation matrix");
+    return SM_OK;
+}
+
+namespace {
+int check_map_args(const sm_handle* h, const double* K, const double* dist, int ndist, const double* R,
+                   const double* P, int width, int height, const float* mx, const float* my, int map_pitch) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!K || !R || !P || !mx || !my || width <= 0 || height <= 0 || map_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad rectify-map arguments");
+    if (!(ndist == 0 || ndist == 4 || ndist == 5 || ndist == 8) || (ndist && !dist))
+        return fail(SM_ERR_INVALID_ARG, "distortion vectors hold 0, 4, 5 or 8 coefficients");
+    return SM_OK;
+}
+}  // namespace
+
+SM_API int sm_init_rectify_map_device(sm_handle* h, const double* K, const double* dist, int ndist, const double* R,
+                                      const double* P, int width, int height, float* d_mapx, float* d_mapy,
+                                      int map_pitch, void* stream) {
+    int rc = check_map_args(h, K, dist, ndist, R, P, width, height, d_mapx, d_mapy, map_pitch);
+    if (rc) return rc;
+    SM_HIP(hipSetDevice(h->device));
+    const hipError_t e = sm::launch_rectify_map(K, dist, ndist, R, P, width, height, d_mapx, d_mapy, map_pitch,
+                                                (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(SM_ERR_INVALID_ARG, "P[:, :3] * R is singular");
+    SM_HIP(e);
+    return SM_OK;
+}
+
+SM_API int sm_init_rectify_map(sm_handle* h, const double* K, const double* dist, int ndist, const double* R,
+                               const double* P, int width, int height, float* mapx, float* mapy, int map_pitch) {
+    int rc = check_map_args(h, K, dist, ndist, R, P, width, height, mapx, mapy, map_pitch);
+    if (rc) return rc;
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t plane = (size_t)width * height;
+    if (h->maps_bytes < 2 * plane * sizeof(float)) {
+        if (h->d_maps) (void)hipFree(h->d_maps);
+        h->d_maps = nullptr;
+        h->maps_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_maps, 2 * plane * sizeof(float)));
+        h->maps_bytes = 2 * plane * sizeof(float);
+    }
+    float* dmx = h->d_maps;
+    float* dmy = h->d_maps + plane;
+    const hipError_t e = sm::launch_rectify_map(K, dist, ndist, R, P, width, height, dmx, dmy, width, s);
+    if (e == hipErrorInvalidValue) return fail(SM_ERR_INVALID_ARG, "P[:, :3] * R is singular");
+    SM_HIP(e);
+    SM_HIP(copy2d(mapx, (size_t)map_pitch * sizeof(float), dmx, width * sizeof(float), width * sizeof(float), height,
+                  hipMemcpyDeviceToHost, s));
+    SM_HIP(copy2d(mapy, (size_t)map_pitch * sizeof(float), dmy, width * sizeof(float), width * sizeof(float), height,
+                  hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
+}
+
 SM_API int sm_ad_volume_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
                                int pitch, int num_disp, uint8_t* d_dif, void* stream) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");

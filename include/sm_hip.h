@@ -162,6 +162,26 @@ SM_API int sm_bgr_to_gray_u8(sm_handle *h, const uint8_t *bgr, int width, int he
 SM_API int sm_remap_u8(sm_handle *h, const uint8_t *src, int width, int height, int pitch, const float *mapx,
                        const float *mapy, int map_pitch, uint8_t *dst, int dst_pitch);
 
+/* ---- rectification maps (the step before the remap) ----
+ * The reference's remapTest (Caller.cpp:27-74) builds its maps with Rectify (Utility.cpp:228-234):
+ * OpenCV 2.4 stereoRectify(K1, D1, K2, D2, size, R, T, R1, R2, P1, P2, Q, CV_CALIB_ZERO_DISPARITY)
+ * (alpha = -1, newImageSize = size) and initUndistortRectifyMap(Kk, Dk, Rk, Pk, size, CV_32FC1).
+ * Matrices are row-major doubles: K 3x3, R 3x3 (r_len 9) or a rotation vector (r_len 3), T 3,
+ * R1/R2 3x3, P1/P2 3x4, Q 4x4.  dist: ndist = 0, 4, 5 or 8 coefficients k1 k2 p1 p2 [k3 [k4 k5 k6]].
+ * sm_stereo_rectify is host-only math (no device, no handle). */
+SM_API int sm_stereo_rectify(const double *K1, const double *dist1, int ndist1, const double *K2,
+                             const double *dist2, int ndist2, int width, int height, const double *R,
+                             int r_len, const double *T, double *R1, double *R2, double *P1, double *P2,
+                             double *Q);
+/* CV_32FC1 maps for one camera on the GPU (map_pitch in floats).  Device form: asynchronous on
+ * `stream`; host form: synchronous, maps staged through the handle. */
+SM_API int sm_init_rectify_map_device(sm_handle *h, const double *K, const double *dist, int ndist,
+                                      const double *R, const double *P, int width, int height,
+                                      float *d_mapx, float *d_mapy, int map_pitch, void *stream);
+SM_API int sm_init_rectify_map(sm_handle *h, const double *K, const double *dist, int ndist,
+                               const double *R, const double *P, int width, int height, float *mapx,
+                               float *mapy, int map_pitch);
+
 /* imread -> cvtColor -> blockMatching_gpu in one call (Caller.cpp:12-19): BGR(A) host frames
  * are uploaded, converted to gray on the GPU and matched.  Synchronous. */
 SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,

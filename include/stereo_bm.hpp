@@ -26,7 +26,10 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iostream>
+#include <sstream>
+#include <string>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -39,6 +42,9 @@
 #ifndef CV_32FC1
 #define CV_32FC1 5
 #endif
+#ifndef CV_64FC1
+#define CV_64FC1 6
+#endif
 
 // the host vector type the reference's callers cast BGR data to (Caller.cpp:92, Device.cuh:52)
 struct uchar3 {
@@ -49,7 +55,7 @@ typedef unsigned char uchar;
 namespace sm {
 
 // Minimal single-channel image (the subset of cv::Mat that the reference's path uses): 8-bit by
-// default, or CV_32FC1 for remap maps (elem = 4).
+// default, CV_32FC1 for remap maps (elem = 4), CV_64FC1 for calibration matrices (elem = 8).
 struct Mat {
     int rows = 0, cols = 0;
     size_t step = 0;                     // bytes per row
@@ -64,7 +70,7 @@ struct Mat {
         : rows(r), cols(c), elem(elem_size(type)), data(static_cast<uint8_t*>(ptr)) {
         step = stp ? stp : (size_t)c * elem;
     }
-    static size_t elem_size(int type) { return type == CV_32FC1 ? 4 : 1; }
+    static size_t elem_size(int type) { return type == CV_64FC1 ? 8 : type == CV_32FC1 ? 4 : 1; }
     void create(int r, int c, int type = CV_8UC1) {
         const size_t e = elem_size(type);
         if (r == rows && c == cols && e == elem && store) return;
@@ -79,6 +85,12 @@ struct Mat {
     template <typename T> const T* ptr(int r = 0) const { return reinterpret_cast<const T*>(data + (size_t)r * step); }
     bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
     size_t total() const { return (size_t)rows * cols; }
+};
+
+struct Size {                            // cv::Size: (width, height)
+    int width = 0, height = 0;
+    Size() = default;
+    Size(int w, int h) : width(w), height(h) {}
 };
 
 namespace detail {
@@ -216,3 +228,125 @@ inline void PreCal(const SmHostMat& left0, const SmHostMat& right0, uchar* dif_,
                         searchRange, dif_) != SM_OK)
         std::cerr << "PreCal: " << sm_last_error_string() << std::endl;
 }
+
+// ---- Utility.h (Utility.h:26-27, :42): the calibration load and Rectify in front of remap_gpu ----
+namespace sm {
+namespace detail {
+
+// Every `name: !!opencv-matrix` node of an OpenCV FileStorage YAML file (the block form
+// FileStorage writes: rows / cols / dt / data: [ ... ]), as CV_64FC1 — LoadDataBatch converts each
+// matrix with convertTo(..., CV_64F), Utility.cpp:29-40.  Values are rounded through float first
+// when dt is 'f', as FileStorage stores them in a CV_32F Mat.
+inline bool read_opencv_matrix(const std::string& text, const std::string& name, Mat& out) {
+    size_t pos = 0;
+    for (;;) {
+        pos = text.find(name, pos);
+        if (pos == std::string::npos) return false;
+        const bool start = pos == 0 || text[pos - 1] == ' ' || text[pos - 1] == '\n' || text[pos - 1] == '\t';
+        size_t q = pos + name.size();
+        while (q < text.size() && text[q] == ' ') ++q;
+        if (start && q < text.size() && text[q] == ':') break;
+        pos = q;
+    }
+    auto field = [&](const char* key) -> std::string {
+        const size_t k = text.find(key, pos);
+        if (k == std::string::npos) return std::string();
+        size_t v = text.find(':', k) + 1;
+        while (v < text.size() && text[v] == ' ') ++v;
+        size_t e = v;
+        while (e < text.size() && text[e] != '\n' && text[e] != '\r') ++e;
+        return text.substr(v, e - v);
+    };
+    const int rows = std::atoi(field("rows").c_str()), cols = std::atoi(field("cols").c_str());
+    const std::string dt = field("dt");
+    const size_t lb = text.find('[', text.find("data", pos)), rb = text.find(']', lb);
+    if (rows <= 0 || cols <= 0 || lb == std::string::npos || rb == std::string::npos) return false;
+    std::string body = text.substr(lb + 1, rb - lb - 1);
+    for (char& c : body)
+        if (c == ',' || c == '\n' || c == '\r') c = ' ';
+    std::istringstream is(body);
+    out.create(rows, cols, CV_64FC1);
+    for (int i = 0; i < rows * cols; ++i) {
+        double v;
+        if (!(is >> v)) return false;
+        out.ptr<double>(i / cols)[i % cols] = (!dt.empty() && dt[0] == 'f') ? (double)(float)v : v;
+    }
+    return true;
+}
+
+template <typename M> inline std::vector<double> to_f64(const M& m) {   // CV_64FC1 Mat -> row-major vector
+    std::vector<double> v;
+    for (int r = 0; r < m.rows; ++r)
+        for (int c = 0; c < m.cols; ++c) v.push_back(reinterpret_cast<const double*>(m.data + (size_t)r * m.step)[c]);
+    return v;
+}
+
+}  // namespace detail
+
+// LoadData (Utility.cpp:17-23): one matrix by name (CV_64FC1).
+inline Mat LoadData(const std::string& filename, const std::string& varName) {
+    std::ifstream f(filename);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    Mat m;
+    if (!detail::read_opencv_matrix(ss.str(), varName, m)) std::cerr << "LoadData: no matrix " << varName << std::endl;
+    return m;
+}
+
+// LoadDataBatch (Utility.cpp:25-42): LeftMat, RightMat, LeftDist, RightDist, RotationVec,
+// TranslationVec, each as CV_64FC1.  Returns false (and says which) when the file or a node is missing.
+inline bool LoadDataBatch(const std::string& filename, Mat& camMat1, Mat& camMat2, Mat& distCoe1, Mat& distCoe2,
+                          Mat& R, Mat& T) {
+    std::ifstream f(filename);
+    if (!f) {
+        std::cerr << "LoadDataBatch: cannot open " << filename << std::endl;
+        return false;
+    }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string text = ss.str();
+    const char* names[6] = {"LeftMat", "RightMat", "LeftDist", "RightDist", "RotationVec", "TranslationVec"};
+    Mat* outs[6] = {&camMat1, &camMat2, &distCoe1, &distCoe2, &R, &T};
+    for (int i = 0; i < 6; ++i)
+        if (!detail::read_opencv_matrix(text, names[i], *outs[i])) {
+            std::cerr << "LoadDataBatch: no matrix " << names[i] << " in " << filename << std::endl;
+            return false;
+        }
+    return true;
+}
+
+// Rectify (Utility.cpp:228-234): stereoRectify(..., CV_CALIB_ZERO_DISPARITY) on the host, then the
+// CV_32FC1 maps of both cameras computed on the GPU (sm_init_rectify_map).  Inputs are CV_64FC1
+// (what LoadDataBatch returns); R is 3x3 or a 3-vector.
+template <typename M, typename F>
+inline int Rectify(const M& camMat1, const M& camMat2, const M& distCoe1, const M& distCoe2, const M& R, const M& T,
+                   Size imageSize, F& mapX1, F& mapY1, F& mapX2, F& mapY2) {
+    const std::vector<double> K1 = detail::to_f64(camMat1), K2 = detail::to_f64(camMat2);
+    const std::vector<double> d1 = detail::to_f64(distCoe1), d2 = detail::to_f64(distCoe2);
+    const std::vector<double> Rv = detail::to_f64(R), Tv = detail::to_f64(T);
+    if (K1.size() != 9 || K2.size() != 9 || Tv.size() != 3 || (Rv.size() != 9 && Rv.size() != 3)) {
+        std::cerr << "Rectify: bad matrix sizes" << std::endl;
+        return SM_ERR_INVALID_ARG;
+    }
+    double R1[9], R2[9], P1[12], P2[12], Q[16];
+    const int w = imageSize.width, h = imageSize.height;
+    int rc = sm_stereo_rectify(K1.data(), d1.empty() ? nullptr : d1.data(), (int)d1.size(), K2.data(),
+                               d2.empty() ? nullptr : d2.data(), (int)d2.size(), w, h, Rv.data(), (int)Rv.size(),
+                               Tv.data(), R1, R2, P1, P2, Q);
+    detail::Engine& e = detail::engine();
+    if (rc == SM_OK && !e.ensure(w, h, 1)) rc = SM_ERR_DEVICE;
+    if (rc == SM_OK) {
+        mapX1.create(h, w, CV_32FC1), mapY1.create(h, w, CV_32FC1), mapX2.create(h, w, CV_32FC1), mapY2.create(h, w, CV_32FC1);
+        rc = sm_init_rectify_map(e.h, K1.data(), d1.empty() ? nullptr : d1.data(), (int)d1.size(), R1, P1, w, h,
+                                 reinterpret_cast<float*>(mapX1.data), reinterpret_cast<float*>(mapY1.data),
+                                 (int)(mapX1.step / sizeof(float)));
+    }
+    if (rc == SM_OK)
+        rc = sm_init_rectify_map(e.h, K2.data(), d2.empty() ? nullptr : d2.data(), (int)d2.size(), R2, P2, w, h,
+                                 reinterpret_cast<float*>(mapX2.data), reinterpret_cast<float*>(mapY2.data),
+                                 (int)(mapX2.step / sizeof(float)));
+    if (rc != SM_OK) std::cerr << "Rectify: " << sm_last_error_string() << std::endl;
+    return rc;
+}
+
+}  // namespace sm

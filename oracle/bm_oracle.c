@@ -69,6 +69,65 @@ ORA_API void ora_remap(const uint8_t *src, int W, int H, const float *mapx, cons
 }
 
 /* ------------------------------------------------------------------------- */
+/* Rectification maps in front of the remap: Rectify (Utility.cpp:228-234)     */
+/* calls initUndistortRectifyMap(K, dist, R1, P1, size, CV_32FC1, mapX, mapY).  */
+/* OpenCV 2.4.12 is a third-party dependency absent from the reference tree;   */
+/* this restates its published imgproc/src/undistort.cpp algorithm:            */
+/*   iR = (P[:, :3] * R)^-1, the 3x3 inverse by OpenCV's adjugate formula       */
+/*        (cv::invert DECOMP_LU for n == 3: det3, d = 1/det, cofactors * d);    */
+/*   per row i: _x = i*ir[1] + ir[2], _y = i*ir[4] + ir[5], _w = i*ir[7] + ir[8],*/
+/*   then per column j (accumulated: _x += ir[0], _y += ir[3], _w += ir[6]):    */
+/*   w = 1/_w, x = _x*w, y = _y*w, r2 = x^2 + y^2,                               */
+/*   kr = (1 + ((k3 r2 + k2) r2 + k1) r2) / (1 + ((k6 r2 + k5) r2 + k4) r2),     */
+/*   u = fx (x kr + p1 2xy + p2 (r2 + 2x^2)) + u0,                              */
+/*   v = fy (y kr + p1 (r2 + 2y^2) + p2 2xy) + v0,   map = ((float)u, (float)v). */
+/* dist holds ndist (0, 4, 5 or 8) coefficients k1 k2 p1 p2 [k3 [k4 k5 k6]].   */
+/* Compiled with -ffp-contract=off, so every product / sum rounds as written.  */
+/* Parity with OpenCV itself is unpinned (no OpenCV here).                     */
+/* ------------------------------------------------------------------------- */
+static void ora_inv3(const double *m, double *t)
+{
+    double d = (m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6])) +
+               m[2] * (m[3] * m[7] - m[4] * m[6]);
+    d = 1. / d;
+    t[0] = (m[4] * m[8] - m[5] * m[7]) * d;
+    t[1] = (m[2] * m[7] - m[1] * m[8]) * d;
+    t[2] = (m[1] * m[5] - m[2] * m[4]) * d;
+    t[3] = (m[5] * m[6] - m[3] * m[8]) * d;
+    t[4] = (m[0] * m[8] - m[2] * m[6]) * d;
+    t[5] = (m[2] * m[3] - m[0] * m[5]) * d;
+    t[6] = (m[3] * m[7] - m[4] * m[6]) * d;
+    t[7] = (m[1] * m[6] - m[0] * m[7]) * d;
+    t[8] = (m[0] * m[4] - m[1] * m[3]) * d;
+}
+
+ORA_API void ora_init_rectify_map(const double *K, const double *dist, int ndist, const double *R,
+                                  const double *P, int W, int H, float *mapx, float *mapy)
+{
+    double k[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ar[9], iR[9];
+    for (int i = 0; i < ndist && i < 8; ++i) k[i] = dist[i];
+    for (int i = 0; i < 3; ++i)          /* Ar = P(:, 0:3) (3x4 row-major), Ar * R */
+        for (int j = 0; j < 3; ++j)
+            ar[i * 3 + j] = ((P[i * 4 + 0] * R[0 * 3 + j]) + P[i * 4 + 1] * R[1 * 3 + j]) + P[i * 4 + 2] * R[2 * 3 + j];
+    ora_inv3(ar, iR);
+    const double u0 = K[2], v0 = K[5], fx = K[0], fy = K[4];
+    const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3], k3 = k[4], k4 = k[5], k5 = k[6], k6 = k[7];
+    for (int i = 0; i < H; ++i) {
+        double _x = i * iR[1] + iR[2], _y = i * iR[4] + iR[5], _w = i * iR[7] + iR[8];
+        for (int j = 0; j < W; ++j, _x += iR[0], _y += iR[3], _w += iR[6]) {
+            double w = 1. / _w, x = _x * w, y = _y * w;
+            double x2 = x * x, y2 = y * y;
+            double r2 = x2 + y2, _2xy = 2 * x * y;
+            double kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2);
+            double u = fx * (x * kr + p1 * _2xy + p2 * (r2 + 2 * x2)) + u0;
+            double v = fy * (y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy) + v0;
+            mapx[(int64_t)i * W + j] = (float)u;
+            mapy[(int64_t)i * W + j] = (float)v;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------- */
 /* a1: absolute-difference volume.                                           */
 /* PreCal BlockMatching.cpp:89-109 / kernalPreCal_V2 Device.cu:19-32:        */
 /*   dif[d][p] = |L[p] - R[p-d]| when (p mod W) >= d, else left at the       */

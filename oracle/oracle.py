@@ -58,6 +58,8 @@ def lib():
         L.ora_remap.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                 ctypes.POINTER(ctypes.c_float), _u8p]
         L.ora_median_u8.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p]
+        L.ora_init_rectify_map.argtypes = [_f64p, _f64p, ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.ora_synth_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
         _lib = L
     return _lib
@@ -201,3 +203,136 @@ def synth_pair(seed: int, W: int, H: int, D: int):
     R = np.empty((H, W), np.uint8)
     lib().ora_synth_pair(ctypes.c_uint64(seed), W, H, D, _p(L, _u8p), _p(R, _u8p))
     return L, R
+
+
+# ---------------------------------------------------------------------------------------------
+# Rectification (the caller-side step before remap: Rectify, BlockMatching/Utility.cpp:228-234,
+# called from remapTest, Caller.cpp:50-51).  The reference delegates to OpenCV 2.4.12's
+# stereoRectify(..., CV_CALIB_ZERO_DISPARITY) with the C++ defaults alpha = -1 and
+# newImageSize = Size(), then initUndistortRectifyMap(..., CV_32FC1).  OpenCV is a third-party
+# dependency absent from the reference tree and from this image; the functions below restate its
+# published calib3d/src/calibration.cpp (cvStereoRectify, cvRodrigues2, cvUndistortPoints,
+# cvProjectPoints2) in numpy, fp64, with the float32 point buffers OpenCV uses (CV_32FC2) rounded
+# where it rounds them.  Parity with OpenCV itself: UNPINNED (no OpenCV output exists here).
+# This numpy formulation is deliberately independent of the product's C++ one
+# (gpu_stereo_matching_amd/csrc/bm_rectify.hip): different SVD, different code.
+# ---------------------------------------------------------------------------------------------
+def rodrigues_to_vec(R: np.ndarray) -> np.ndarray:
+    """cvRodrigues2 3x3 -> 3x1: orthogonalise by SVD (R = U V^T), then axis * angle."""
+    U, _, Vt = np.linalg.svd(np.asarray(R, np.float64))
+    R = U @ Vt
+    rx, ry, rz = R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]
+    s = np.sqrt((rx * rx + ry * ry + rz * rz) * 0.25)
+    c = min(1.0, max(-1.0, (R[0, 0] + R[1, 1] + R[2, 2] - 1) * 0.5))
+    theta = np.arccos(c)
+    if s < 1e-5:
+        if c > 0:
+            return np.zeros(3)
+        t = (R + np.eye(3)) * 0.5          # theta ~ pi (OpenCV's branch)
+        rx, ry, rz = (np.sqrt(max(t[i, i], 0.0)) for i in range(3))
+        if R[0, 1] < 0:
+            ry = -ry
+        if R[0, 2] < 0:
+            rz = -rz
+        if abs(rx) < abs(ry) and abs(rx) < abs(rz) and (R[1, 2] > 0) != (ry * rz > 0):
+            rz = -rz
+        v = np.array([rx, ry, rz])
+        return v * (theta / np.linalg.norm(v))
+    return np.array([rx, ry, rz]) * (theta / (2 * s))
+
+
+def rodrigues_to_mat(r: np.ndarray) -> np.ndarray:
+    """cvRodrigues2 3x1 -> 3x3: R = cos I + (1 - cos) n n^T + sin [n]x."""
+    r = np.asarray(r, np.float64).reshape(3)
+    theta = np.linalg.norm(r)
+    if theta < np.finfo(np.float64).eps:
+        return np.eye(3)
+    n = r / theta
+    c, s = np.cos(theta), np.sin(theta)
+    nx = np.array([[0, -n[2], n[1]], [n[2], 0, -n[0]], [-n[1], n[0], 0]])
+    return c * np.eye(3) + (1 - c) * np.outer(n, n) + s * nx
+
+
+def undistort_points(pts: np.ndarray, K: np.ndarray, dist: np.ndarray) -> np.ndarray:
+    """cvUndistortPoints with R = P = 0: 5 fixed-point iterations (k1..k6, p1, p2), normalised
+    output stored as float32 (the CV_32FC2 buffer of cvStereoRectify)."""
+    k = np.zeros(8)
+    k[:len(dist)] = dist
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    out = np.empty_like(pts, dtype=np.float32)
+    for i, (u, v) in enumerate(pts.astype(np.float64)):
+        x0 = x = (u - cx) * (1.0 / fx)
+        y0 = y = (v - cy) * (1.0 / fy)
+        for _ in range(5 if len(dist) else 0):
+            r2 = x * x + y * y
+            icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2)
+            dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x)
+            dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y
+            x = (x0 - dx) * icdist
+            y = (y0 - dy) * icdist
+        out[i] = (x, y)
+    return out
+
+
+def stereo_rectify(K1, dist1, K2, dist2, width: int, height: int, R, T):
+    """cvStereoRectify, flags = CV_CALIB_ZERO_DISPARITY, alpha = -1, newImageSize = imageSize.
+    R is a 3x3 rotation matrix or a 3-vector; returns (R1, R2, P1, P2, Q) as float64 arrays."""
+    K1, K2 = np.asarray(K1, np.float64).reshape(3, 3), np.asarray(K2, np.float64).reshape(3, 3)
+    dist1, dist2 = np.asarray(dist1, np.float64).ravel(), np.asarray(dist2, np.float64).ravel()
+    R = np.asarray(R, np.float64)
+    T = np.asarray(T, np.float64).reshape(3)
+    nx, ny = float(width), float(height)
+    om = rodrigues_to_vec(R) if R.size == 9 else R.reshape(3)
+    r_r = rodrigues_to_mat(om * -0.5)                 # half rotation for each camera
+    t = r_r @ T
+    idx = 0 if abs(t[0]) > abs(t[1]) else 1
+    c = t[idx]
+    nt = np.linalg.norm(t)
+    uu = np.zeros(3)
+    uu[idx] = 1.0 if c > 0 else -1.0
+    ww = np.cross(t, uu)
+    nw = np.linalg.norm(ww)
+    if nw > 0.0:
+        ww = ww * (np.arccos(abs(c) / nt) / nw)
+    wR = rodrigues_to_mat(ww)
+    R1 = wR @ r_r.T
+    R2 = wR @ r_r
+    t = R2 @ T
+    fc_new = np.inf
+    for K, dk in ((K1, dist1), (K2, dist2)):
+        dk1 = dk[0] if len(dk) else 0.0
+        fc = K[idx ^ 1, idx ^ 1]
+        if dk1 < 0:
+            fc *= 1 + dk1 * (nx * nx + ny * ny) / (4 * fc * fc)
+        fc_new = min(fc_new, fc)
+    cc = []
+    for K, dk, Rk in ((K1, dist1, R1), (K2, dist2, R2)):
+        pts = np.array([[(i % 2) * (nx - 1), (i // 2) * (ny - 1)] for i in range(4)], np.float32)
+        und = undistort_points(pts, K, dk).astype(np.float64)
+        X = np.concatenate([und, np.ones((4, 1))], axis=1)       # convertPointsHomogeneous (float32 values)
+        Y = X @ Rk.T
+        proj = np.stack([fc_new * Y[:, 0] / Y[:, 2], fc_new * Y[:, 1] / Y[:, 2]], 1).astype(np.float32)
+        avg = proj.astype(np.float64).mean(axis=0)
+        cc.append([(nx - 1) / 2 - avg[0], (ny - 1) / 2 - avg[1]])
+    cx = (cc[0][0] + cc[1][0]) * 0.5                 # CV_CALIB_ZERO_DISPARITY
+    cy = (cc[0][1] + cc[1][1]) * 0.5
+    cx, cy = nx * cx / nx, ny * cy / ny              # newImgSize == imageSize rescale (rounds)
+    P1 = np.array([[fc_new, 0, cx, 0], [0, fc_new, cy, 0], [0, 0, 1, 0]], np.float64)
+    P2 = P1.copy()
+    P2[idx, 3] = t[idx] * fc_new
+    Q = np.array([[1, 0, 0, -cx], [0, 1, 0, -cy], [0, 0, 0, fc_new], [0, 0, -1.0 / t[idx], (cx - cx) / t[idx]]], np.float64)
+    return R1, R2, P1, P2, Q
+
+
+def init_rectify_map(K, dist, R, P, width: int, height: int):
+    """initUndistortRectifyMap(..., CV_32FC1) in the C restatement (fp64, OpenCV's op order)."""
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    dist = np.ascontiguousarray(dist, np.float64).ravel()
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    P = np.ascontiguousarray(P, np.float64).reshape(12)
+    mx = np.empty((height, width), np.float32)
+    my = np.empty((height, width), np.float32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib().ora_init_rectify_map(_p(K, _f64p), _p(dist, _f64p), int(dist.size), _p(R, _f64p), _p(P, _f64p),
+                               width, height, mx.ctypes.data_as(fp), my.ctypes.data_as(fp))
+    return mx, my

@@ -43,24 +43,33 @@ def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):
 
 
 @pytest.mark.gpu
-def test_remap_test_cpp(tmp_path, gray, oracle):
-    """remapTest() -> remap_gpu(Mat&...) (Device.cuh:51) against the CPU_Remap restatement."""
-    L, R = gray["Art/view1"], gray["Art/view5"]
+def test_remap_test_cpp(tmp_path, oracle):
+    """remapTest() (Caller.cpp:27-74) end to end through stereo_bm.hpp: LoadDataBatch of the reference's
+    calibration YAML -> Rectify (stereoRectify + GPU maps) -> remap_gpu on the Chess/Set2 pair at
+    320x200.  Maps bit-exact with the oracle's initUndistortRectifyMap on the same R/P, and both
+    rectified views bit-exact with the CPU_Remap restatement."""
+    from gpu_stereo_matching_amd import calib
+    chess = np.load(os.path.join(ROOT, "tests", "golden", "chess_set2_gray.npz"))
+    L, R = chess["Left_320x200"], chess["Right_320x200"]
     H, W = L.shape
-    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
-    th = np.float32(0.03)
-    mapx = (np.cos(th) * xx - np.sin(th) * yy + np.float32(3.25)).astype(np.float32)
-    mapy = (np.sin(th) * xx + np.cos(th) * yy - np.float32(7.5)).astype(np.float32)
+    yml = os.path.join(ROOT, "tests", "golden", "Calib_Data_OpenCV.yml")
     _write_pgm(tmp_path / "l.pgm", L)
     _write_pgm(tmp_path / "r.pgm", R)
-    mapx.tofile(tmp_path / "mx.f32")
-    mapy.tofile(tmp_path / "my.f32")
     env = dict(os.environ, SM_DEMO="remapTest", SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
-               SM_MAPX=str(tmp_path / "mx.f32"), SM_MAPY=str(tmp_path / "my.f32"), SM_OUT=str(tmp_path / "o.pgm"))
+               SM_CALIB=yml, SM_OUT=str(tmp_path / "o.pgm"), SM_OUT2=str(tmp_path / "o2.pgm"),
+               SM_MAPS=str(tmp_path / "maps.f32"))
     r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "GPU Remap : " in r.stdout
-    assert np.array_equal(_read_pgm(tmp_path / "o.pgm"), oracle.remap(L, mapx, mapy))
+    K1, K2, d1, d2, Rm, T = calib.load_data_batch(yml)
+    R1, R2, P1, P2, _ = calib.stereo_rectify(K1, d1, K2, d2, (W, H), Rm, T)
+    mx1, my1 = oracle.init_rectify_map(K1, d1, R1, P1, W, H)
+    mx2, my2 = oracle.init_rectify_map(K2, d2, R2, P2, W, H)
+    maps = np.fromfile(tmp_path / "maps.f32", np.float32).reshape(4, H, W)
+    for got, want in zip(maps, (mx1, my1, mx2, my2)):
+        assert np.array_equal(got, want)
+    assert np.array_equal(_read_pgm(tmp_path / "o.pgm"), oracle.remap(L, mx1, my1))
+    assert np.array_equal(_read_pgm(tmp_path / "o2.pgm"), oracle.remap(R, mx2, my2))
 
 
 @pytest.mark.gpu
