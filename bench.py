@@ -365,7 +365,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
-            "ms_per_frame": round(lat, 4) if lat is not None else None,
+            "ms_per_frame": round(ms_per_step / B, 4),             # per-GPU throughput time (value's inverse at N=1)
+            "latency_ms_batch1": round(lat, 4) if lat is not None else None,   # one frame per launch
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
