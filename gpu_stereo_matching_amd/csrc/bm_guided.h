@@ -12,4 +12,14 @@ hipError_t launch_guided_match(const uint8_t* L, const uint8_t* R, int W, int H,
                                int64_t frame_stride, int radius, int D, float eps, int valid_mode, uint8_t* disp,
                                int out_pitch, int64_t out_frame_stride, hipStream_t s);
 
+// Same, with the fused right view (valid_mode 0 only): the right-view disparity of STMatching's rule
+// C_R(y, u, d) = C_L(y, u + d, d), strict < from d = 0, no threshold (StereoHelper.cpp:131-180), is
+// written to `right` ([batch][H][rpitch], frame stride rstride).  gpart: per-tile right-key
+// partials, guided_right_partial_bytes(...) bytes.  gpart == nullptr: left view only.
+hipError_t launch_guided_match_lr(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                  int64_t frame_stride, int radius, int D, float eps, int valid_mode, uint8_t* disp,
+                                  int out_pitch, int64_t out_frame_stride, int* gpart, uint8_t* right, int rpitch,
+                                  int64_t rstride, hipStream_t s);
+size_t guided_right_partial_bytes(int W, int H, int radius, int D, int batch);
+
 }  // namespace sm

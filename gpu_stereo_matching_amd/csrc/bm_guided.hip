@@ -22,6 +22,21 @@
 // iteration runs {S1V(d), S2V(d-1)} | barrier | {S1H(d), S2H(d-1)} | barrier: two workgroup
 // barriers per d instead of four.  The guide statistics (SI = sum L, SII = sum L^2, N) come from
 // S1V/S1H on AD := L (R band read as 0), once per tile.
+//
+// Fused right view (RIGHT = true, the LR check): STMatching derives the right-view cost from the
+// left one, C_R(y, u, d) = C_L(y, u + d, d) (GetRightMatchingCostFromLeft, StereoHelper.cpp:156-180),
+// and takes its WTA with strict < from d = 0 and no threshold (StereoHelper.cpp:131-154).  S2H makes
+// every output's q (= N*q / N) at disparity d a candidate for the right pixel u = x - d:
+//   key = (int)(q * 2^14) << 8 | position      (q clamped to [-512, 512), truncated: error < 6.2e-5)
+// and keeps, per thread, one key slot per output; slot j holds u = xs + j - d at step d.  After each
+// step the top slot can gain nothing more from this segment: it is passed to the next segment of
+// the row (the lane to its right, DPP row_shr:1) whose new bottom slot is that same u.  The last
+// segment of the row writes it to HBM (gpart), and guided_right_reduce_kernel takes the minimum
+// over the ~(D + 8 SW2) / TW tiles covering each u.  The position field is the output column within
+// the tile, kept relative to the current segment (+ SW2 * (7 - s)) so that keys created in this
+// segment need no per-lane constant; each hop subtracts SW2.  Ties (equal keys) resolve to the
+// smaller column, i.e. the smaller d, as the reference's strict < does.
+#include <climits>
 #include <type_traits>
 
 #include "bm_common.h"
@@ -100,15 +115,21 @@ struct GeoF {
     static constexpr int LDS = CS_BYTES + MM_BYTES + AB_BYTES + RB_BYTES;
 };
 
-// r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere
-template <int R>
-constexpr int kGuidedWavesPerEU = (R >= 6) ? 2 : 3;
+// r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere; with the fused right
+// view r = 3 (7 outputs per S2H thread) spills at 168 and also runs at 2
+template <int R, bool RIGHT>
+constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && R == 3)) ? 2 : 3;
 
-template <int R>
-__global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kernel(
+// right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
+constexpr float kRightScale = 16384.0f;
+constexpr float kRightMax = 8388607.0f;    // 2^23 - 1
+constexpr float kRightMin = -8388608.0f;   // -2^23
+
+template <int R, bool RIGHT>
+__global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride, int tiles_x,
-    int tiles) {
+    int tiles, int* __restrict__ gpart, int K) {
     using G = GeoF<R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
@@ -179,9 +200,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         asm volatile("" : "+v"(off));
         v2col[k] = reinterpret_cast<const float2*>(reinterpret_cast<const uint8_t*>(abp) + off);
     }
-    // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2); rows run across lanes
-    // (measured 2 % faster than segments across lanes)
-    const int h2r = tid & 31, h2s = tid >> 5;
+    // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2).  Rows run across lanes
+    // (measured 2 % faster than segments across lanes), except with the fused right view, whose
+    // key chain runs from each segment to the next lane: lane = segment + 8 * row.
+    const int h2r = RIGHT ? (tid >> 3) : (tid & 31);
+    const int h2s = RIGHT ? (tid & 7) : (tid >> 5);
     const int oy = y0 + h2r;
 
     // per-A-pixel constants (filled by the stats pass) and per-output WTA state.
@@ -193,6 +216,10 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     float fSI[G::SW1], invden[G::SW1], invN[G::SW1];
     float oI[G::SW2], bq[G::SW2];
     int bdd[G::SW2], dlim[G::SW2];
+    // fused right view: 2^14 / N per output (NaN for outputs outside the image or the tile, whose
+    // keys then clamp to the maximum), and the key slots
+    float rinv[RIGHT ? G::SW2 : 1];
+    int rk[RIGHT ? G::SW2 : 1];
 #pragma unroll
     for (int o = 0; o < G::SW2; ++o) {
         const int x = x0 + h2s * G::SW2 + o;
@@ -201,7 +228,25 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
         dlim[o] = valid_mode == 0 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
+        if constexpr (RIGHT) {
+            rinv[o] = ok ? kRightScale / (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_nanf("");
+            rk[o] = INT_MAX;
+        }
     }
+    // right-key chain: first / last segment of the row, this row's partial-key column in gpart
+    const bool seg_first = h2s == 0, seg_last = h2s == 7;
+    int* gdst = RIGHT ? gpart + ((int64_t)frame * tiles + t) * K * G::TH + h2r : nullptr;
+    auto chain_step = [&](int k) {
+        if constexpr (RIGHT) {
+            const int leaving = rk[G::SW2 - 1];
+#pragma unroll
+            for (int j = G::SW2 - 1; j > 0; --j) rk[j] = rk[j - 1];
+            // row_shr:1 = lane - 1, i.e. the previous segment of the same row (lane 8r + s)
+            const int in = __builtin_amdgcn_update_dpp(INT_MAX, leaving, 0x111, 0xF, 0xF, false) - G::SW2;
+            rk[0] = seg_first ? INT_MAX : in;
+            if (seg_last) gdst[(int64_t)k * G::TH] = leaving;
+        }
+    };
 
     // ================= S1V =================
     // STATS: the guide statistics pass, AD := L (the R band read as 0)
@@ -335,10 +380,18 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
             const bool take = (!LIM || d <= dlim[o]) && q < bq[o];
             bq[o] = take ? q : bq[o];
             bdd[o] = take ? d : bdd[o];
+            if constexpr (RIGHT) {
+                // candidate for right pixel u = x - d (slot o): q = (N q) / N, fixed point, position
+                // 7 SW2 + o (the output column relative to this segment, see the file header)
+                const float qs = __builtin_fmaxf(__builtin_fminf(q * rinv[o], kRightMax), kRightMin);
+                const int key = ((int)qs << 8) | (7 * G::SW2 + o);
+                rk[o] = key < rk[o] ? key : rk[o];
+            }
             const float2 vout = row[o];
             sa -= vout.x;
             sb -= vout.y;
         }
+        chain_step(d);
     };
 
     s1v(0, std::true_type{}, std::false_type{});
@@ -365,6 +418,10 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
         }
         __syncthreads();
     }
+    // drain the right-key chain: 8 SW2 - 1 more steps move every slot out through the last segment
+    if constexpr (RIGHT) {
+        for (int k = D; k < K; ++k) chain_step(k);
+    }
     uint8_t* Df = disp + (int64_t)frame * ostride;
 #pragma unroll
     for (int o = 0; o < G::SW2; ++o) {
@@ -374,16 +431,80 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R>)) void guided_fused_kerne
     }
 }
 
+// Right view of the fused pass: for each right pixel u of a tile row band, the minimum key over the
+// tiles whose chain emitted u (k = x0 + SPAN - 1 - u in [0, K)), decoded to d = x0 + position - u.
+// Block = 64 columns x the 32 rows of one tile band; reads are 128-B rows of gpart ([k][row]).
+__global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __restrict__ gpart, int tiles_x, int tiles,
+                                                                  int TW, int SPAN, int K, int W, int H,
+                                                                  uint8_t* __restrict__ right, int rpitch,
+                                                                  int64_t rstride) {
+    constexpr int TH = 32, UC = 64;
+    __shared__ uint8_t band[TH][UC];
+    const int u0 = blockIdx.x * UC, ty = blockIdx.y, f = blockIdx.z;
+    const int* base = gpart + ((int64_t)f * tiles + (int64_t)ty * tiles_x) * K * TH;
+    for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
+        const int j = e & (TH - 1), ul = e >> 5, u = u0 + ul;
+        int dr = 0;
+        if (u < W) {
+            const int n = u - SPAN + 1;
+            const int tlo = n <= 0 ? 0 : (n + TW - 1) / TW;
+            const int thi = min(tiles_x - 1, (u - SPAN + K) / TW);
+            // keys order (cost, column) within a tile only: across tiles compare the cost field,
+            // strict <, in ascending tile order, so equal costs keep the smaller column = smaller d
+            int best = base[((int64_t)tlo * K + (tlo * TW + SPAN - 1 - u)) * TH + j], bx = tlo * TW;
+            for (int tx = tlo + 1; tx <= thi; ++tx) {
+                const int k = tx * TW + SPAN - 1 - u;
+                const int key = base[((int64_t)tx * K + k) * TH + j];
+                if ((key >> 8) < (best >> 8)) {
+                    best = key;
+                    bx = tx * TW;
+                }
+            }
+            dr = bx + (best & 0xFF) - u;
+        }
+        band[j][ul] = (uint8_t)dr;
+    }
+    __syncthreads();
+    uint8_t* Rf = right + (int64_t)f * rstride;
+    for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
+        const int j = e >> 6, ul = e & (UC - 1);
+        const int y = ty * TH + j, u = u0 + ul;
+        if (y < H && u < W) Rf[(int64_t)y * rpitch + u] = band[j][ul];
+    }
+}
+
 template <int R>
 hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch,
-                     int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride, hipStream_t s) {
+                     int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride, int* gpart,
+                     uint8_t* right, int rpitch, int64_t rstride, hipStream_t s) {
     using G = GeoF<R>;
     const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((guided_fused_kernel<R>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg, W,
-                       H, pitch, fstride, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y);
+    if (!gpart) {
+        hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L,
+                           Rimg, W, H, pitch, fstride, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
+                           tiles_x * tiles_y, nullptr, 0);
+        return hipGetLastError();
+    }
+    const int span = 8 * G::SW2;
+    const int K = D + span - 1;
+    hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg,
+                       W, H, pitch, fstride, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
+                       K);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(guided_right_reduce_kernel, dim3((unsigned)((W + 63) / 64), (unsigned)tiles_y, (unsigned)batch),
+                       dim3(256), 0, s, gpart, tiles_x, tiles_x * tiles_y, G::TW, span, K, W, H, right, rpitch,
+                       rstride);
     return hipGetLastError();
+}
+
+template <int R>
+size_t partial_bytes(int W, int H, int D, int batch) {
+    using G = GeoF<R>;
+    const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
+    return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }
 
 }  // namespace
@@ -391,9 +512,35 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
 hipError_t launch_guided_match(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                                int64_t frame_stride, int radius, int D, float eps, int valid_mode, uint8_t* disp,
                                int out_pitch, int64_t out_frame_stride, hipStream_t s) {
+    return launch_guided_match_lr(L, R, W, H, pitch, batch, frame_stride, radius, D, eps, valid_mode, disp, out_pitch,
+                                  out_frame_stride, nullptr, nullptr, 0, 0, s);
+}
+
+size_t guided_right_partial_bytes(int W, int H, int radius, int D, int batch) {
+#define SM_GUIDED_BYTES(r) \
+    case r: return partial_bytes<r>(W, H, D, batch)
+    switch (radius) {
+        SM_GUIDED_BYTES(0);
+        SM_GUIDED_BYTES(1);
+        SM_GUIDED_BYTES(2);
+        SM_GUIDED_BYTES(3);
+        SM_GUIDED_BYTES(4);
+        SM_GUIDED_BYTES(5);
+        SM_GUIDED_BYTES(6);
+        SM_GUIDED_BYTES(7);
+        default: return 0;
+    }
+#undef SM_GUIDED_BYTES
+}
+
+hipError_t launch_guided_match_lr(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                  int64_t frame_stride, int radius, int D, float eps, int valid_mode, uint8_t* disp,
+                                  int out_pitch, int64_t out_frame_stride, int* gpart, uint8_t* right, int rpitch,
+                                  int64_t rstride, hipStream_t s) {
     if (D < 1 || D > kMaxDisp) return hipErrorInvalidValue;
+    if (gpart && (!right || valid_mode != 0)) return hipErrorInvalidValue;
 #define SM_GUIDED_CASE(r) \
-    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, D, eps, valid_mode, disp, out_pitch, out_frame_stride, s)
+    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, D, eps, valid_mode, disp, out_pitch, out_frame_stride, gpart, right, rpitch, rstride, s)
     switch (radius) {
         SM_GUIDED_CASE(0);
         SM_GUIDED_CASE(1);

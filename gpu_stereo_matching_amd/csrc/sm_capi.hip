@@ -169,8 +169,9 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
 // Core device-side pass over `batch` frames.  Workspace planes (d_lr) are dense W x H frames.
 //   left map  : matched straight into `disp`, or into a workspace plane when SM_MEDIAN filters it
 //               into `disp` afterwards (StereoDisparity.cpp:85/119);
-//   right map : fused with the left pass for box r <= 7, else matched on the mirrored
-//               pair (valid d <= x, no threshold) and kept mirrored;
+//   right map : fused with the left pass for box r <= 7 and for guided (right keys from
+//               the left costs, bm_guided.hip); box r > 7 matches the mirrored pair (valid d <= x,
+//               no threshold) and keeps it mirrored;
 //   LR check  : StereoDisparity.cpp:136-147 on the (median-filtered, :119-126) maps.
 int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
@@ -182,6 +183,7 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     const int64_t P = (int64_t)W * H;
     const int64_t PB = P * batch;
     const bool fused_right = lr && !guided && radius <= sm::kMaxFastRadius;
+    const bool guided_right = lr && guided;   // right view fused into the guided pass (bm_guided.hip)
     if ((flags & SM_STAGED) != 0) {
         if (guided || lr || radius > sm::kMaxFastRadius)
             return fail(SM_ERR_INVALID_ARG, "SM_STAGED supports box aggregation without LR, radius <= %d",
@@ -190,7 +192,8 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     }
 
     // workspace: [left raw (med)] [right (lr)] [right filtered (lr && med)] [mirrored L, R (lr, not fused)]
-    const int64_t n_planes = (med ? 1 : 0) + (lr ? 1 : 0) + (lr && med ? 1 : 0) + (lr && !fused_right ? 2 : 0);
+    const bool mirrored = lr && !fused_right && !guided_right;
+    const int64_t n_planes = (med ? 1 : 0) + (lr ? 1 : 0) + (lr && med ? 1 : 0) + (mirrored ? 2 : 0);
     if (n_planes > 0) {
         int rc = ensure_lr(h, (size_t)(n_planes * PB));
         if (rc) return rc;
@@ -202,7 +205,7 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     if (lr) ws += PB;
     uint8_t* right_med = (lr && med) ? ws : nullptr;
     if (lr && med) ws += PB;
-    uint8_t* mL = (lr && !fused_right) ? ws : nullptr;
+    uint8_t* mL = mirrored ? ws : nullptr;
     uint8_t* mR = mL ? mL + PB : nullptr;
 
     // ---- left map ----
@@ -236,6 +239,11 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
             return SM_OK;
         }
         SM_HIP(sm::launch_box_match_lr(a, batch, 0, right_map, nullptr, W, P, s));
+    } else if (guided_right) {
+        int rc = ensure_rpart(h, sm::guided_right_partial_bytes(W, H, radius, D, batch));
+        if (rc) return rc;
+        SM_HIP(sm::launch_guided_match_lr(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
+                                         lstride, reinterpret_cast<int*>(h->d_rpart), right_map, W, P, s));
     } else if (guided) {
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
@@ -245,14 +253,11 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     if (med) SM_HIP(sm::launch_median(left_raw, W, H, W, P, batch, kMedianRadius, disp, opitch, ostride, s));
     if (!lr) return SM_OK;
 
-    // ---- right map on the mirrored pair (StereoHelper.cpp:156-180 + :131-154) ----
-    if (!fused_right) {
+    // ---- right map on the mirrored pair (StereoHelper.cpp:156-180 + :131-154), box r > 7 ----
+    if (mirrored) {
         SM_HIP(sm::launch_mirror(R, W, H, pitch, fstride, batch, mL, W, P, s));
         SM_HIP(sm::launch_mirror(L, W, H, pitch, fstride, batch, mR, W, P, s));
-        if (guided) {
-            SM_HIP(sm::launch_guided_match(mL, mR, W, H, W, batch, P, radius, D, h->guided_eps, 1, right_map, W, P,
-                                          s));
-        } else {
+        {
             sm::MatchArgs b = a;
             b.left = mL;
             b.right = mR;
@@ -272,7 +277,7 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
         SM_HIP(sm::launch_median(right_map, W, H, W, P, batch, kMedianRadius, right_med, W, P, s));
         rcheck = right_med;
     }
-    SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rcheck, W, P, fused_right ? 0 : 1, W, H, batch, disp, opitch,
+    SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rcheck, W, P, mirrored ? 1 : 0, W, H, batch, disp, opitch,
                                ostride, right_out, mask_out, apitch, astride, s));
     return SM_OK;
 }

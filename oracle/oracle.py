@@ -163,6 +163,32 @@ def box_lr(left, right, radius: int, D: int):
     return disp, rdisp, checked, mask
 
 
+def right_cost_from_left(cost: np.ndarray) -> np.ndarray:
+    """GetRightMatchingCostFromLeft (STMatching/StereoHelper.cpp:156-180) on a [D][H][W] float volume:
+    C_R(y, u, d) = C_L(y, u + d, d) if u + d < W, else C_R(y, u, d - 1)."""
+    cost = np.asarray(cost, np.float64)
+    D, H, W = cost.shape
+    out = np.empty_like(cost)
+    u = np.arange(W)
+    prev = None
+    for d in range(D):
+        src = np.minimum(u + d, W - 1)
+        cur = cost[d][:, src]
+        if prev is not None:
+            cur = np.where((u + d < W)[None, :], cur, prev)
+        out[d] = cur
+        prev = cur
+    return out
+
+
+def right_wta_float(cost: np.ndarray):
+    """Right-view WTA (StereoHelper.cpp:131-154: strict < from d = 0, no threshold) of the right
+    cost derived from a float left volume.  Returns (right disparity, C_R volume, best C_R)."""
+    cr = right_cost_from_left(cost)
+    disp = np.argmin(cr, axis=0).astype(np.uint8)   # first minimum = strict < from d = 0
+    return disp, cr, cr.min(axis=0)
+
+
 def guided_disp(left, right, radius: int, D: int, eps: float, want_q: bool = False):
     """fp64 guided-filter aggregation (this build's definition; parity unpinned)."""
     left, right = _img(left), _img(right)

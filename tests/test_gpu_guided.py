@@ -51,12 +51,48 @@ def test_guided_synthetic_ragged(matcher, oracle, W, H, D, r):
     assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
 
 
-def test_guided_lr(matcher, gray):
-    """Guided + LR: the occlusion rule applied to guided left/right maps (checked map is a
-    subset of the left map, occluded pixels 0)."""
+def _check_guided_lr(matcher, oracle, L, R, r, D):
+    """Guided + LR with the right view fused into the guided pass: the right map is STMatching's
+    WTA of C_R(y, u, d) = C_L(y, u + d, d) (StereoHelper.cpp:131-180) on the guided left costs.
+    Left and right maps are judged tie-aware against the fp64 oracle (the right keys also carry the
+    2^-14 fixed-point quantisation, far inside TOL); the checked map and mask must equal the
+    reference's LR rule (StereoDisparity.cpp:136-147) applied to the returned maps, bit for bit."""
+    from guided_check import TOL
+    H, W = L.shape
+    disp_o, q, best = oracle.guided_disp(L, R, r, D, EPS, want_q=True)
+    left = matcher.match(L, R, r, D, agg="guided")
+    ok, _ = tie_aware_check(left, q, {"disp": disp_o, "best": best}, D, W)
+    assert ok.all(), f"left: {int((~ok).sum())} pixels outside the tie-aware tolerance"
+    chk, rd, mask = matcher.match_lr(L, R, r, D, agg="guided")
+    rd_o, cr, best_r = oracle.right_wta_float(q)
+    ys, us = np.mgrid[0:H, 0:W]
+    assert (rd < D).all()
+    cost_g = cr[rd.astype(np.int64), ys, us]
+    ok_r = (rd == rd_o) | (cost_g <= best_r + TOL)
+    assert ok_r.all(), f"right: {int((~ok_r).sum())} pixels outside the tie-aware tolerance"
+    assert (rd == rd_o).mean() > 0.99
+    chk_o, mask_o = oracle.lr_check(left, rd)
+    assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+    return mask
+
+
+@pytest.mark.parametrize("r,D", [(5, 64), (3, 48), (0, 16), (7, 32), (1, 100)])
+def test_guided_lr_art(matcher, oracle, gray, r, D):
     L, R = gray["Art_/view1"], gray["Art_/view5"]
-    left = matcher.match(L, R, 5, 64, agg="guided")
-    chk, rd, mask = matcher.match_lr(L, R, 5, 64, agg="guided")
-    assert ((chk == 0) | (chk == left)).all()
-    assert (chk[mask == 1] == left[mask == 1]).all()
+    mask = _check_guided_lr(matcher, oracle, L, R, r, D)
     assert 0.3 < mask.mean() < 1.0
+
+
+@pytest.mark.parametrize("W,H,D,r", [(333, 77, 100, 4), (64, 20, 8, 1), (21, 13, 30, 2), (97, 40, 256, 5),
+                                     (130, 33, 64, 6)])
+def test_guided_lr_synthetic_ragged(matcher, oracle, W, H, D, r):
+    L, R = oracle.synth_pair(W * 3 + H, W, H, max(D, 16))
+    _check_guided_lr(matcher, oracle, L, R, r, D)
+
+
+def test_guided_lr_flat(matcher, oracle):
+    """All-equal images: every cost is 0, so the first d wins everywhere in both views."""
+    L = np.full((40, 90), 77, np.uint8)
+    chk, rd, mask = matcher.match_lr(L, L.copy(), 5, 32, agg="guided")
+    assert (rd == 0).all()
+    assert (mask == 0).all() and (chk == 0).all()     # d == 0 counts as occluded (StereoDisparity.cpp:141)

@@ -143,3 +143,16 @@ def test_median_restatement_matches_numpy(oracle, r, W, H):
     w = sliding_window_view(p, (k, k)).reshape(H, W, k * k)
     want = np.sort(w, axis=2)[:, :, (k * k) // 2]
     assert np.array_equal(oracle.median(a, r), want)
+
+
+def test_right_wta_float_matches_int_restatement(oracle, gray):
+    """The float right-view WTA used for the guided LR check (numpy) == the C restatement of
+    StereoHelper.cpp:131-180 on the integer box costs of a bundled pair."""
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    _, cost = oracle.box_disp(L, R, 4, 48, want_cost=True)
+    rd_f, cr, best = oracle.right_wta_float(cost.astype(np.float64))
+    assert np.array_equal(rd_f, oracle.right_wta(cost))
+    H, W = L.shape
+    u = W - 5                                    # clamp rule: C_R(u, d) = C_R(u, d-1) for u + d >= W
+    assert np.array_equal(cr[10:, :, u], np.repeat(cr[4:5, :, u], 38, axis=0))
+    assert np.array_equal(best, cr.min(axis=0))
