@@ -101,11 +101,12 @@ struct GeoF {
     static constexpr int CSS_B = CSS0 + ((NSEG1 * SW1 - CSS0) % 32 + 32) % 32;
     static constexpr int CSS_OLD = CSS0 + 1;
     static constexpr int lds_for(int css) {
-        return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + TH * AW * 8 +
+        return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + TH * (AW | 1) * 8 +
                AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
     }
     static constexpr int CSS = (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : 53248)) ? CSS_B : CSS_OLD;
-    static constexpr int MS = AW;                            // float2 per mm row
+    // float2 per mm row: odd, so that S2H's ds_read_b64 of 32 rows (one per lane) tile all 64 banks
+    static constexpr int MS = AW | 1;
     static constexpr int ABS = NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW;   // float2 per a/b row
     static constexpr int RBW = 64 + kBandChunk;              // right band bytes per P row (one d-chunk)
     static constexpr int CS_BYTES = ((AHP * CSS * 4 > PHP * 64 ? AHP * CSS * 4 : PHP * 64) + 15) & ~15;  // lt aliases cs
@@ -181,14 +182,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     const bool h1_on = tid < G::AH * G::NSEG1;
     const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
     const int h1y = y0 - R + h1i;
-    // S1H's a/b row segment, its LDS offset pinned in a VGPR: the compiler otherwise re-adds the
-    // region offset before every store (ds_write2 offsets are 8-bit)
-    float2* h1dst;
-    {
-        uint32_t off = (uint32_t)(reinterpret_cast<uint8_t*>(abp + h1i * G::ABS + h1s * G::SW1) - smem);
-        asm volatile("" : "+v"(off));
-        h1dst = reinterpret_cast<float2*>(smem + off);
-    }
+    // S1H's a/b row segment as an LDS byte address (the kernel has no static LDS, so the dynamic
+    // block starts at 0).  The stores are written as ds_write_b64 with immediate offsets: 8-B
+    // aligned, serviced in 16-lane groups, where thread tid writes bank pair 9 tid + c (mod 16) at
+    // r = 5 (distinct within each group).  The compiler's ds_write2_b32 for a float2 store was 2-way
+    // conflicted on the (a/4) mod 32 write banks.
+    uint32_t h1off = (uint32_t)(reinterpret_cast<uint8_t*>(abp + h1i * G::ABS + h1s * G::SW1) - smem);
     // S2V ownership: A column v2j = lane, output rows [8*v2g, 8*v2g + 8) with v2g = wave (one row
     // group per wave: its lanes read one contiguous a/b row span, no bank conflicts at a wrap)
     const bool v2_on = lane < G::AW;
@@ -306,7 +305,6 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     auto s1h = [&]() {
         if (!h1_on) return;
         const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
-        float2* dst = h1dst;
         // the whole segment is loaded before the first a/b store (the compiler cannot tell abp
         // from cs, so interleaved loads would each wait for the stores before them)
         uint32_t v[G::SW1 + 2 * R];
@@ -330,7 +328,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             asm("v_mad_i32_i24 %0, %1, %2, %0" : "+v"(num) : "v"(nN[o]), "v"(sip));
             const float a = (float)num * invden[o];
             const float b = __builtin_fmaf(-a, fSI[o], (float)sp) * invN[o];
-            dst[o] = make_float2(a, b);
+            // one ds_write_b64 (the compiler emits ds_write2_b32 for a float2 store here)
+            asm volatile("ds_write_b64 %0, %1 offset:%2"
+                         :
+                         : "v"(h1off), "v"(__builtin_bit_cast(double, make_float2(a, b))), "i"(8 * o)
+                         : "memory");
             sp -= v[o] >> 20;
             sip -= v[o] & kPLow;
         }
