@@ -11,9 +11,10 @@ that are already resident in HBM when the timed region starts.
 
 Multi-GPU: one process per GPU.  The path partitions by frame (independent pairs), so ranks
 shard frames with no data-path collective ("scaling": "weak").  The two single-frame modes of
-SURVEY §8e are measured in the same run for N > 1: "dslice" (each rank owns a disparity slice of
-the SAME frame, packed-key MIN all-reduce over RCCL) and "rowband" (each rank owns a band of rows
-plus an r-row halo, all-gather of the uint8 bands).
+SURVEY §8e are measured in the same run for N > 1: "dslice" (cfg4: each rank owns a disparity
+slice of the SAME 1080p d_max=256 frame; packed-key MIN reduce-scatter + uint8 all-gather over
+RCCL, and the plain MIN all-reduce beside it) and "rowband" (each rank owns a band of rows plus an
+r-row halo, all-gather of the uint8 bands).
 
 Rank 0 prints ONE JSON line.  Timing: barrier + synchronize on both sides of exactly K steps,
 max over ranks.  The dominant kernel's duration is measured live with HIP events on the stream
@@ -295,31 +296,35 @@ def main():
         torch.cuda.synchronize(dev)
         lat = e0.elapsed_time(e1) / 50
 
-    # ---- d-slice sharding of one frame with an RCCL MIN all-reduce (N > 1) ----
+    # ---- d-slice sharding of one frame (N > 1): cfg4, 1080p d_max=256, MIN reduction of the slice keys ----
     dslice = rowband = None
     if distributed:
         from gpu_stereo_matching_amd import sharding
-        keys = torch.empty((H, W), dtype=torch.int32, device=dev)
+        D4 = 256
+        keys, dflat = sharding.dslice_buffers(H, W, world, dev)
         d1 = torch.empty((H, W), dtype=torch.uint8, device=dev)
-
-        def dstep():
-            sharding.match_dslice(m, Lt[0], Rt[0], r, D, rank, world, keys_t=keys, out_t=d1, stream=stream)
-
-        for _ in range(5):
-            dstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
         n = max(10, args.steps // 4)
-        t1 = time.perf_counter()
-        for _ in range(n):
-            dstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        dslice = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
-                  "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_reduce MIN int32 ({backend})",
-                  "keys_bytes_per_frame": W * H * 4, "scaling": "strong"}
+        dslice = {"config": f"cfg4: {W}x{H} d_max={D4} r={r}, one frame d-sharded over {world} ranks",
+                  "unit": "disparity-maps/s", "scaling": "strong", "keys_bytes_per_frame": W * H * 4}
+        for coll, label in (("rs_ag", f"reduce_scatter MIN int32 + all_gather uint8 ({backend})"),
+                            ("allreduce", f"all_reduce MIN int32 ({backend})")):
+            def dstep():
+                sharding.match_dslice(m, Lt[0], Rt[0], r, D4, rank, world, keys_t=keys, out_t=dflat, stream=stream,
+                                      collective=coll)
+
+            for _ in range(5):
+                dstep()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t1 = time.perf_counter()
+            for _ in range(n):
+                dstep()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            dslice[coll] = {"value": round(n / float(dt.item()), 2), "ms_per_frame": round(float(dt.item()) * 1000 / n, 4),
+                            "collective": label}
 
         # row bands of one frame (r-row halo, all-gather of uint8 bands)
         def bstep():

@@ -4,9 +4,13 @@ Three ways to spread the work over ranks:
   * frames (independent rectified pairs): each rank matches its own frames; no collective in the
     data path — the path's natural partition, used for the headline maps/s ("scaling": "weak");
   * disparity slices of ONE frame: rank k scans d in [k*D/G, (k+1)*D/G) and emits per-pixel
-    packed keys (SAD << 8 | d); an elementwise MIN all-reduce (RCCL over xGMI on GPUs, gloo on
-    CPU) gives the global argmin with the reference's smallest-d tie break (strict <,
-    Device.cu:57); the threshold / no-match rule is applied after the reduction;
+    packed keys (SAD << 8 | d); an elementwise MIN gives the global argmin with the reference's
+    smallest-d tie break (strict <, Device.cu:57); the threshold / no-match rule is applied after
+    the reduction.  Default collective: MIN reduce-scatter of the 4-byte keys, each rank turns
+    its 1/G of the pixels into uint8 disparities, all-gather of those bytes — 5P(G-1)/G bytes
+    through each rank's links instead of the 8P(G-1)/G of a MIN all-reduce of the keys (xGMI
+    is point-to-point, so the ring collectives are per-link bound: SURVEY §8e).  RCCL over xGMI
+    on GPUs, gloo on CPU;
   * row bands of ONE frame: rank k owns output rows [k*ceil(H/G), ...) and matches them from its
     rows plus a halo (r rows for box windows, 2r for the guided filter's two nested windows, +3
     with the 7x7 median post-filter);
@@ -36,9 +40,21 @@ def seed_key(radius: int) -> int:
     return (50 * win * win) << 8
 
 
+def _host_staged(group) -> bool:
+    """gloo takes CPU tensors only for some collectives: device tensors are staged through host
+    copies there (the rehearsal mode of bench.py, several ranks on one GPU).  RCCL works in place."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
 def reduce_slice_keys(keys, group=None):
     """In-place MIN all-reduce of an int32 key map (keys < 2^31 by construction)."""
     import torch.distributed as dist
+    if keys.is_cuda and _host_staged(group):
+        h = keys.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MIN, group=group)
+        keys.copy_(h)
+        return keys
     dist.all_reduce(keys, op=dist.ReduceOp.MIN, group=group)
     return keys
 
@@ -50,20 +66,95 @@ def keys_to_disparity_host(keys, radius: int):
     return np.where((k >> 8) < (seed_key(radius) >> 8), k & 0xFF, 0).astype(np.uint8)
 
 
-def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int, world: int,
-                 keys_t=None, out_t=None, stream=None, group=None):
-    """One frame, d-sharded over the process group: slice keys -> MIN all-reduce -> disparity."""
+def padded_pixels(height: int, width: int, world: int) -> int:
+    """Pixels rounded up to a multiple of the world size (the reduce-scatter chunking)."""
+    return -(-(height * width) // world) * world
+
+
+def dslice_buffers(height: int, width: int, world: int, device):
+    """(flat int32 keys, flat uint8 disparity) of padded_pixels(...) elements for match_dslice."""
     import torch
+    n = padded_pixels(height, width, world)
+    return (torch.empty(n, dtype=torch.int32, device=device), torch.empty(n, dtype=torch.uint8, device=device))
+
+
+def reduce_scatter_keys(keys_flat, world: int, group=None):
+    """MIN reduce-scatter of a flat padded key map: this rank's 1/world chunk of the global minimum."""
+    import torch
+    import torch.distributed as dist
+    chunk = torch.empty(keys_flat.numel() // world, dtype=keys_flat.dtype, device=keys_flat.device)
+    if keys_flat.is_cuda and _host_staged(group):
+        h = chunk.cpu()
+        dist.reduce_scatter_tensor(h, keys_flat.cpu(), op=dist.ReduceOp.MIN, group=group)
+        return chunk.copy_(h)
+    dist.reduce_scatter_tensor(chunk, keys_flat, op=dist.ReduceOp.MIN, group=group)
+    return chunk
+
+
+def gather_disparity(chunk_u8, out_flat, group=None):
+    """All-gather of the per-rank uint8 disparity chunks into the flat padded map."""
+    import torch.distributed as dist
+    if out_flat.is_cuda and _host_staged(group):
+        h = out_flat.cpu()
+        dist.all_gather_into_tensor(h, chunk_u8.cpu(), group=group)
+        return out_flat.copy_(h)
+    dist.all_gather_into_tensor(out_flat, chunk_u8, group=group)
+    return out_flat
+
+
+def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int, world: int,
+                 keys_t=None, out_t=None, stream=None, group=None, collective: str = "rs_ag"):
+    """One frame, d-sharded over the process group: slice keys -> MIN reduce -> disparity.
+
+    collective "rs_ag" (default): reduce-scatter the keys, convert this rank's chunk, all-gather
+    uint8; "allreduce": MIN all-reduce of the whole key map, then convert.  keys_t / out_t: the
+    flat buffers of dslice_buffers() (allocated when None).  Returns the [H, W] disparity."""
+    import torch
+    if collective not in ("rs_ag", "allreduce"):
+        raise ValueError("collective must be 'rs_ag' or 'allreduce'")
     lo, hi = dslice_bounds(num_disp, rank, world)
     H, W = left_t.shape[-2:]
-    if keys_t is None:
-        keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+    P = H * W
+    if keys_t is None or out_t is None:
+        keys_t, out_t = dslice_buffers(H, W, world, left_t.device)
+    if keys_t.numel() != padded_pixels(H, W, world) or out_t.numel() != keys_t.numel():
+        raise ValueError("keys_t / out_t must be dslice_buffers(H, W, world)")
+    keys_img = keys_t[:P].view(H, W)
     if hi > lo:
-        matcher.slice_keys_device(left_t, right_t, radius, lo, hi, keys_t=keys_t, stream=stream)
+        matcher.slice_keys_device(left_t, right_t, radius, lo, hi, keys_t=keys_img, stream=stream)
     else:
-        keys_t.fill_(seed_key(radius))
-    reduce_slice_keys(keys_t, group)
-    return matcher.keys_to_disp_device(keys_t, radius, out_t=out_t, stream=stream)
+        keys_img.fill_(seed_key(radius))
+    keys_t[P:].fill_(seed_key(radius))
+    if stream is not None:
+        torch.cuda.current_stream(left_t.device).wait_stream(stream)
+    if collective == "allreduce":
+        reduce_slice_keys(keys_t, group)
+        matcher.keys_to_disp_device(keys_t.view(1, -1), radius, out_t=out_t.view(1, -1))
+        return out_t[:P].view(H, W)
+    chunk = reduce_scatter_keys(keys_t, world, group)
+    n = chunk.numel()
+    mine = matcher.keys_to_disp_device(chunk.view(1, n), radius)
+    gather_disparity(mine.view(n), out_t, group)
+    return out_t[:P].view(H, W)
+
+
+def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_ag", group=None):
+    """CPU (gloo) form of match_dslice's reduction for tests: this rank's [H, W] slice keys (int32
+    numpy) -> the [H, W] uint8 disparity of the global minimum, through the same collectives."""
+    import numpy as np
+    import torch
+    H, W = keys.shape
+    P = H * W
+    flat = torch.full((padded_pixels(H, W, world),), seed_key(radius), dtype=torch.int32)
+    flat[:P] = torch.from_numpy(np.ascontiguousarray(keys, np.int32).reshape(P))
+    if collective == "allreduce":
+        reduce_slice_keys(flat, group)
+        return keys_to_disparity_host(flat.numpy()[:P].view(np.uint32), radius).reshape(H, W)
+    chunk = reduce_scatter_keys(flat, world, group)
+    mine = torch.from_numpy(keys_to_disparity_host(chunk.numpy().view(np.uint32), radius))
+    out = torch.empty(flat.numel(), dtype=torch.uint8)
+    gather_disparity(mine, out, group)
+    return out.numpy()[:P].reshape(H, W)
 
 
 def band_rows(height: int, rank: int, world: int) -> Tuple[int, int]:

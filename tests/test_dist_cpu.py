@@ -33,10 +33,9 @@ def _worker(rank, world, port, W, H, r, D, result_dir):
         keys = O.box_keys_slice(L, R, r, lo, hi).view(np.int32)
     else:
         keys = np.full((H, W), sharding.seed_key(r), np.int32)
-    kt = torch.from_numpy(keys.copy())
-    sharding.reduce_slice_keys(kt)
-    disp = sharding.keys_to_disparity_host(kt.numpy().view(np.uint32), r)
-    np.save(os.path.join(result_dir, f"disp{rank}.npy"), disp)
+    for coll in ("allreduce", "rs_ag"):
+        disp = sharding.match_dslice_host_keys(keys, r, world, collective=coll)
+        np.save(os.path.join(result_dir, f"disp{rank}_{coll}.npy"), disp)
     # frame-parallel: every frame handled exactly once across ranks
     mine = torch.zeros(10, dtype=torch.int64)
     for f in sharding.frame_shard(10, rank, world):
@@ -46,16 +45,19 @@ def _worker(rank, world, port, W, H, r, D, result_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,D", [(2, 64), (2, 7), (3, 64)])
-def test_dslice_min_allreduce_gloo(tmp_path, world, D):
-    W, H, r = 120, 40, 3
+@pytest.mark.parametrize("world,D,W", [(2, 64, 120), (2, 7, 120), (3, 64, 121), (4, 3, 77)])
+def test_dslice_min_reduction_gloo(tmp_path, world, D, W):
+    """Both d-slice reductions (MIN all-reduce; MIN reduce-scatter + uint8 all-gather, with the
+    pixel count padded to the world size) give the full-range disparity on every rank."""
+    H, r = 40, 3
     port = _free_port()
     mp.spawn(_worker, args=(world, port, W, H, r, D, str(tmp_path)), nprocs=world, join=True)
     from oracle import oracle as O
     L, R = O.synth_pair(4321, W, H, max(D, 16))
     want = O.box_disp(L, R, r, D)
     for k in range(world):
-        assert np.array_equal(np.load(tmp_path / f"disp{k}.npy"), want)
+        for coll in ("allreduce", "rs_ag"):
+            assert np.array_equal(np.load(tmp_path / f"disp{k}_{coll}.npy"), want), (k, coll)
         assert (np.load(tmp_path / f"frames{k}.npy") == 1).all()
 
 
@@ -63,7 +65,8 @@ def test_shard_helpers():
     assert sharding.dslice_bounds(128, 0, 8) == (0, 16)
     assert sharding.dslice_bounds(128, 7, 8) == (112, 128)
     assert sum(len(sharding.frame_shard(13, k, 4)) for k in range(4)) == 13
-    assert sharding.dslice_bounds(3, 5, 8)[0] == sharding.dslice_bounds(3, 5, 8)[1] or True
+    assert sharding.dslice_bounds(3, 4, 8) == (1, 1)   # more ranks than disparities: empty slice
+    assert sharding.padded_pixels(40, 121, 3) == 4842 and sharding.padded_pixels(40, 120, 3) == 4800
 
 
 def _band_worker(rank, world, port, W, H, r, D, mode, result_dir):
