@@ -1,8 +1,8 @@
 // bm_staged.hip — the staged (cost-volume) formulation of the box path:
 //   K1 ad_volume_kernel (bm_volume.hip): AD volume, u8 [D][H][W]               P*D bytes written
 //   K2 box_sad_kernel:  SAD volume, u16 [D][H][W]: the (2r+1)^2 window sum of each AD plane,
-//                       zero-padded at the borders (= the clipped window, Device.cu:46-56)
-//                                                                               P*D read, 2*P*D written
+//                       zero-padded at the borders (= the clipped window, Device.cu:46-56);
+//                       column strips walked top to bottom    P*D read (+2r rows per band), 2*P*D written
 //   K3 volume_wta_kernel: first d with the smallest SAD below 50*win^2, valid d <= W-x
 //                       (Device.cu:37-63); 0 where none                          2*P*D read, P written
 // The fused box_match_kernel computes the same map without the volumes; this chain streams them
@@ -15,12 +15,19 @@
 namespace sm {
 namespace {
 
-constexpr int kST = 256;
-constexpr int kSW = 64, kSH = 32;   // K2 output tile
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// K2: one (64 x 32) tile of one d plane per block.  The input tile is staged with dword loads;
-// vertical running sums (lane = column, the 32 rows in 3 chunks so ~all threads work) go to LDS,
-// then horizontal running sums, 8 outputs per thread written as one 16-B store.
+constexpr int kST = 256;
+constexpr int kSC = 4 * kST;       // K2: input columns per strip (4 per thread)
+constexpr int kSO = kSC - 16;      // K2: output columns per strip (the strip starts 8 columns early)
+constexpr int kSadBlocks = 4096;  // K2 blocks per launch (2048 measured 10 % slower, 8192 the same)
+
+// K2: one column strip x one row band of one d plane per block.  A thread owns 4 input columns
+// and walks the band's rows once: vertical window sums run in registers (two packed u16 pairs,
+// the rows leaving the window kept in a register ring of 2r+1 dwords), each output row's
+// vertical sums go to LDS, and each thread forms 4 horizontal window sums from its neighbours'
+// columns.  Every AD byte is read once per band (the 2r halo rows of a band are re-read;
+// >= ~64-row bands), every SAD value written once as part of an 8-B store.
 __device__ __forceinline__ uint32_t ld4z(const uint8_t* plane, int y, int x, int W, int H) {
     if (y < 0 || y >= H) return 0u;
     const uint8_t* row = plane + (int64_t)y * W;
@@ -37,103 +44,137 @@ __device__ __forceinline__ uint32_t ld4z(const uint8_t* plane, int y, int x, int
 }
 
 template <int R>
-__global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict__ ad, int W, int H, int tiles_x,
+__global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict__ ad, int W, int H, int rows_per_band,
                                                       uint16_t* __restrict__ sad) {
-    constexpr int IW = kSW + 2 * R, IH = kSH + 2 * R;
-    constexpr int IWD = (IW + 3) / 4;                 // dwords per staged row
-    constexpr int CH = 3, CR = (kSH + CH - 1) / CH;   // vertical pass: 3 chunks of <= 11 output rows
-    __shared__ __attribute__((aligned(16))) uint8_t tin[IH][IWD * 4 + 4];
-    __shared__ uint16_t vs[kSH][IW + 2];
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, d = blockIdx.y;
-    const int x0 = tx * kSW, y0 = ty * kSH;
+    constexpr int K = 2 * R + 1;
+    __shared__ __attribute__((aligned(16))) uint16_t vs[2][kSC + 16];
+    const int t = threadIdx.x;
+    const int sx = blockIdx.x, d = blockIdx.z;
+    const int yo0 = blockIdx.y * rows_per_band;
+    const int yo1 = min(H, yo0 + rows_per_band);
+    if (yo0 >= H) return;                               // block-uniform
     const int64_t P = (int64_t)W * H;
     const uint8_t* plane = ad + (int64_t)d * P;
-    for (int e = threadIdx.x; e < IH * IWD; e += kST) {
-        const int i = e / IWD, j = e - (e / IWD) * IWD;
-        *reinterpret_cast<uint32_t*>(&tin[i][4 * j]) = ld4z(plane, y0 - R + i, x0 - R + 4 * j, W, H);
-    }
-    __syncthreads();
-    if (threadIdx.x < CH * IW) {
-        const int j = threadIdx.x % IW, c = threadIdx.x / IW;
-        const int r0 = c * CR, r1 = r0 + CR < kSH ? r0 + CR : kSH;
-        uint32_t sv = 0;
+    uint16_t* outp = sad + (int64_t)d * P;
+    const int xs = sx * kSO;                            // first output column of the strip
+    const int xin = xs - 8 + 4 * t;                     // this thread's 4 input columns
+    const bool vec_out = ((W & 3) == 0) && ((reinterpret_cast<uintptr_t>(sad) & 7) == 0);
+    // vertical sums: E = (col0, col2), O = (col1, col3) as u16 pairs (<= (2r+1) * 255)
+    uint32_t E = 0u, O = 0u, ring[K];
 #pragma unroll
-        for (int i = 0; i < 2 * R; ++i) sv += tin[r0 + i][j];
-        for (int rr = r0; rr < r1; ++rr) {
-            sv += tin[rr + 2 * R][j];
-            vs[rr][j] = (uint16_t)sv;        // <= (2r+1) * 255, fits u16
-            sv -= tin[rr][j];
+    for (int j = 0; j < K; ++j) ring[j] = 0u;
+    const int yi_end = yo1 + R;                         // input rows [yo0 - R, yo1 + R)
+    int buf = 0;
+    for (int base = yo0 - R; base < yi_end; base += K) {
+        // ring slot j holds row base + j - K (this loop's row base + j replaces it)
+        uint32_t nw[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) nw[j] = (base + j < yi_end) ? ld4z(plane, base + j, xin, W, H) : 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int yi = base + j;
+            if (yi >= yi_end) break;                    // block-uniform
+            const uint32_t v = nw[j], o = ring[j];
+            ring[j] = v;
+            E += (v & 0x00FF00FFu) - (o & 0x00FF00FFu);
+            O += ((v >> 8) & 0x00FF00FFu) - ((o >> 8) & 0x00FF00FFu);
+            const int yo = yi - R;                      // window [yi - 2R, yi] is centred on yo
+            if (yo < yo0) continue;                     // warm-up rows of the band
+            uint16_t* row = vs[buf];
+            *reinterpret_cast<uint2*>(row + 4 * t) =
+                make_uint2(__builtin_amdgcn_perm(O, E, 0x05040100u), __builtin_amdgcn_perm(O, E, 0x07060302u));
+            __syncthreads();
+            // outputs xs + 4t + k (k < 4): window of vs indices [4t + 8 + k - R, 4t + 8 + k + R]
+            uint32_t w[12];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const uint2 x2 = *reinterpret_cast<const uint2*>(row + 4 * t + 4 * q);
+                w[2 * q] = x2.x;
+                w[2 * q + 1] = x2.y;
+            }
+            auto val = [&](int i) -> uint32_t { return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu); };
+            uint32_t sum = 0;
+#pragma unroll
+            for (int i = 8 - R; i <= 8 + R; ++i) sum += val(i);
+            uint32_t res[4];
+            res[0] = sum;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                sum += val(8 + R + k) - val(8 - R + k - 1);
+                res[k] = sum;                           // <= (2r+1)^2 * 255 < 2^16 for r <= 7
+            }
+            const int x = xs + 4 * t;
+            if (4 * t < kSO && x < W) {
+                uint16_t* dst = outp + (int64_t)yo * W + x;
+                if (vec_out && x + 4 <= W) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+                } else {
+                    for (int k = 0; k < 4 && x + k < W; ++k) dst[k] = (uint16_t)res[k];
+                }
+            }
+            buf ^= 1;                                   // the next row's sums go to the other buffer
         }
-    }
-    __syncthreads();
-    const int r = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * R; ++k) s += vs[r][c0 + k];
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        s += vs[r][c0 + k + 2 * R];
-        const uint32_t v = s;                // <= (2r+1)^2 * 255 < 2^16 for r <= 7
-        if (k & 1) o[k >> 1] |= v << 16; else o[k >> 1] = v;
-        s -= vs[r][c0 + k];
-    }
-    const int y = y0 + r, x = x0 + c0;
-    if (y >= H) return;
-    uint16_t* dst = sad + (int64_t)d * P + (int64_t)y * W + x;
-    if (x + 8 <= W && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
-        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-    } else {
-        for (int k = 0; k < 8 && x + k < W; ++k) dst[k] = (uint16_t)(o[k >> 1] >> (16 * (k & 1)));
     }
 }
 
-// K3: 4 pixels per thread, 8-B loads of the u16 SAD planes.
+// K3: 8 pixels per thread, one 16-B nontemporal load per d plane (the volume is streamed once and
+// is larger than the MALL).
 __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restrict__ sad, int W, int H, int D,
                                                          uint32_t seed_key, uint8_t* __restrict__ disp,
                                                          int out_pitch) {
+    constexpr int NPX = 8;
     const int64_t P = (int64_t)W * H;
-    const int64_t p0 = ((int64_t)blockIdx.x * kST + threadIdx.x) * 4;
+    const int64_t p0 = ((int64_t)blockIdx.x * kST + threadIdx.x) * NPX;
     if (p0 >= P) return;
-    const int n = P - p0 < 4 ? (int)(P - p0) : 4;
-    int xs[4];
-    uint32_t best[4];
+    const int n = P - p0 < NPX ? (int)(P - p0) : NPX;
+    int lim[NPX];
+    uint32_t best[NPX];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        xs[k] = (int)((p0 + k) % W);
+    for (int k = 0; k < NPX; ++k) {
+        lim[k] = W - (int)((p0 + k) % W);            // validity: d <= W - x (Device.cu:44)
         best[k] = seed_key;
     }
-    const bool vec = n == 4 && ((p0 & 3) == 0) && ((reinterpret_cast<uintptr_t>(sad) & 7) == 0) && ((P & 3) == 0);
+    const bool vec = n == NPX && ((reinterpret_cast<uintptr_t>(sad) & 15) == 0) && ((P & 7) == 0);
     for (int d = 0; d < D; ++d) {
         const uint16_t* pl = sad + (int64_t)d * P + p0;
-        uint32_t s[4];
+        uint32_t s[NPX];
         if (vec) {
-            const uint2 v = *reinterpret_cast<const uint2*>(pl);
-            s[0] = v.x & 0xFFFFu; s[1] = v.x >> 16; s[2] = v.y & 0xFFFFu; s[3] = v.y >> 16;
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pl));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s[2 * q] = v[q] & 0xFFFFu;
+                s[2 * q + 1] = v[q] >> 16;
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) s[k] = k < n ? pl[k] : 0u;
+            for (int k = 0; k < NPX; ++k) s[k] = k < n ? pl[k] : 0u;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < NPX; ++k) {
             const uint32_t key = (s[k] << 8) | (uint32_t)d;
-            // validity: d <= W - x (the `col + d > cols` break, Device.cu:44)
-            best[k] = (d <= W - xs[k] && key < best[k]) ? key : best[k];
+            best[k] = (d <= lim[k] && key < best[k]) ? key : best[k];
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NPX; ++k) {
         if (k >= n) break;
         const int64_t p = p0 + k;
-        const int y = (int)(p / W);
-        disp[(int64_t)y * out_pitch + xs[k]] = best[k] < seed_key ? (uint8_t)(best[k] & 0xFFu) : (uint8_t)0;
+        const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+        disp[(int64_t)y * out_pitch + x] = best[k] < seed_key ? (uint8_t)(best[k] & 0xFFu) : (uint8_t)0;
     }
 }
 
 template <int R>
 hipError_t launch_box_sad_r(const uint8_t* ad, int W, int H, int D, uint16_t* sad, hipStream_t s) {
-    const int tiles_x = (W + kSW - 1) / kSW, tiles_y = (H + kSH - 1) / kSH;
-    hipLaunchKernelGGL(box_sad_kernel<R>, dim3(tiles_x * tiles_y, D), dim3(kST), 0, s, ad, W, H, tiles_x, sad);
+    const int strips = (W + kSO - 1) / kSO;
+    // ~kSadBlocks blocks, bands of >= 32 rows (the 2r halo rows of a band are read twice)
+    int bands = (kSadBlocks + strips * D - 1) / (strips * D);
+    const int max_bands = (H + 31) / 32;
+    bands = bands < 1 ? 1 : (bands > max_bands ? max_bands : bands);
+    const int rows = (H + bands - 1) / bands;
+    bands = (H + rows - 1) / rows;
+    if (D > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(box_sad_kernel<R>, dim3(strips, bands, D), dim3(kST), 0, s, ad, W, H, rows, sad);
     return hipGetLastError();
 }
 
@@ -159,7 +200,7 @@ hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, in
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, uint32_t seed_key, uint8_t* disp,
                              int out_pitch, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
-    const int64_t blocks = (P + 4 * kST - 1) / (4 * kST);
+    const int64_t blocks = (P + 8 * kST - 1) / (8 * kST);
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     hipLaunchKernelGGL(volume_wta_kernel, dim3((unsigned)blocks), dim3(kST), 0, s, sad, W, H, D, seed_key, disp,
                        out_pitch);

@@ -42,9 +42,18 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     const uint8_t* lr = L + (int64_t)f * fstride + (int64_t)y * pitch;
     const uint8_t* rr = R + (int64_t)f * fstride + (int64_t)y * pitch;
     const int nseg = (W + 15) >> 4;
-    for (int x = threadIdx.x; x < kVPad + nseg * 16 + 4; x += kVT) {
-        const int c = x - kVPad;
-        rrow[x] = (c >= 0 && c < W) ? rr[c] : (uint8_t)0;
+    // stage the R row as dwords: rrow dword j = R bytes 4j - 16 .. 4j - 13 (0 outside the row)
+    for (int j = threadIdx.x; j < (kVPad + nseg * 16 + 4) / 4; j += kVT) {
+        const int c = 4 * j - kVPad;
+        uint32_t v = 0;
+        if (c >= 0 && c + 3 < W) {
+            __builtin_memcpy(&v, rr + c, 4);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (c + b >= 0 && c + b < W) v |= (uint32_t)rr[c + b] << (8 * b);
+        }
+        reinterpret_cast<uint32_t*>(rrow)[j] = v;
     }
     __syncthreads();
     const int64_t P = (int64_t)W * H;
@@ -57,15 +66,19 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     if (g >= groups) return;
     const int x0 = seg * 16;
     uint32_t l[4];
+    if (x0 + 16 <= W) {
+        __builtin_memcpy(l, lr + x0, 16);
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
+        for (int q = 0; q < 4; ++q) {
+            uint32_t v = 0;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int x = x0 + 4 * q + b;
-            v |= (x < W ? (uint32_t)lr[x] : 0u) << (8 * b);
+            for (int b = 0; b < 4; ++b) {
+                const int x = x0 + 4 * q + b;
+                v |= (x < W ? (uint32_t)lr[x] : 0u) << (8 * b);
+            }
+            l[q] = v;
         }
-        l[q] = v;
     }
 #pragma unroll 2
     for (int d = d_begin + g; d < d_end; d += groups) {

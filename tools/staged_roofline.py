@@ -9,7 +9,8 @@ P = W * H
 out = os.path.join(ROOT, "gpurun_out", "staged_roofline")
 env = dict(os.environ, TMPDIR="/tmp")
 drv = [sys.executable, os.path.join(ROOT, "tools", "kernel_driver.py"), "--agg", "box-staged", "--batch", "1",
-       "--iters", "10"]
+       "--iters", "10"] + (["--lib", os.environ["SM_LIB"]] if os.environ.get("SM_LIB") else [])
+out = out + os.environ.get("SM_TAG", "")
 subprocess.run(["timeout", "-k", "10", "240", "rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(out, "kt"),
                 "-o", "k", "--output-format", "csv", "--"] + drv, check=True, env=env,
                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -40,5 +41,6 @@ for name, t in dur.items():
 tot = sum(v["avg_ms"] for v in res["kernels"].values())
 res["staged_ms_per_frame"] = round(tot, 4)
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", "staged_roofline_1080p.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", "staged_roofline_1080p%s.json" % os.environ.get("SM_TAG", "")), "w"),
+          indent=1)
 print(json.dumps(res, indent=1))
