@@ -138,6 +138,22 @@ def run_variants(sm, torch, dev, stream, seed):
             "ms_per_frame": round(ms, 4), "achieved_GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 3),
             "bytes_per_frame": W * H * (D + 2)}
         del vol
+        # the reference's two-kernel data flow through HBM volumes (SM_STAGED: AD u8 -> SAD u16 -> WTA),
+        # bit-exact with the fused kernel; every byte of the three volumes crosses HBM
+        o1 = torch.empty_like(Lt)
+        for _ in range(2):
+            m.match_device(Lt, Rt, 5, D, out_t=o1, agg="box-staged", stream=stream)
+        e0.record(stream)
+        for _ in range(10):
+            m.match_device(Lt, Rt, 5, D, out_t=o1, agg="box-staged", stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / 10
+        nbytes = W * H * (D + 2) + 3 * W * H * D + (2 * W * H * D + W * H)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out["staged box 1080p 11x11 d128 (AD u8 -> SAD u16 -> WTA through HBM, HBM-bound)"] = {
+            "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "achieved_GBs": round(gbs, 1),
+            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 3), "bytes_per_frame": nbytes}
         # host frame stream, PCIe-inclusive: FrameStream overlaps H2D / match / D2H on three streams;
         # frames are produced in place in the pinned slots (next_inputs) and consumed in place
         # (callback), so no host-side copy is timed
