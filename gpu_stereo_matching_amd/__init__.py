@@ -17,7 +17,7 @@ All compute runs in ``libsm_hip.so``; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -27,7 +27,7 @@ from .synth import synth_pair  # noqa: F401
 from .gray import bgr_to_gray  # noqa: F401
 
 __all__ = [
-    "BlockMatcher", "blockMatching_gpu", "block_matching_gpu", "SMError", "synth_pair", "bgr_to_gray",
+    "BlockMatcher", "BlockMatcherGroup", "blockMatching_gpu", "block_matching_gpu", "SMError", "synth_pair", "bgr_to_gray",
     "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "SM_MEDIAN", "version",
 ]
 
@@ -295,6 +295,87 @@ class BlockMatcher:
         _capi.check(self._lib.sm_keys_to_disp_device(self._h, keys_t.data_ptr(), W, H, radius, out_t.data_ptr(), W,
                                                      self._stream_ptr(stream)))
         return out_t
+
+
+class BlockMatcherGroup:
+    """Several GPUs driven from this process through the C ABI's group handle (``sm_create_group``):
+    one frame in row bands (one band per device, bit-identical to a single-device pass), or a batch
+    of frames spread over the devices.  ``devices`` may repeat an index (several handles on one GPU)."""
+
+    def __init__(self, devices: Sequence[int], max_width: int = 1920, max_height: int = 1080, max_disp: int = 256):
+        self._lib = _capi.load()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        g = ctypes.c_void_p()
+        _capi.check(self._lib.sm_create_group(len(devices), devs, max_width, max_height, max_disp, ctypes.byref(g)))
+        self._g = g
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "_g", None) is not None and self._g.value:
+            self._lib.sm_destroy_group(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __len__(self):
+        n = ctypes.c_int()
+        _capi.check(self._lib.sm_group_size(self._g, ctypes.byref(n)))
+        return n.value
+
+    def set_guided_eps(self, eps: float):
+        _capi.check(self._lib.sm_group_set_param_f(self._g, _capi.SM_PARAM_GUIDED_EPS, float(eps)))
+
+    def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
+              median: bool = False) -> np.ndarray:
+        """One frame, row-banded over the group (sm_group_block_match_u8)."""
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        if L.shape != R.shape:
+            raise ValueError("left/right sizes differ")
+        H, W = L.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_group_block_match_u8(self._g, L.ctypes.data, R.ctypes.data, W, H, W, radius,
+                                                      num_disp, _flags(agg, lr_check, median), out.ctypes.data, W))
+        return out
+
+    def match_lr(self, left, right, radius: int, num_disp: int, agg: str = "box", median: bool = False
+                 ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(checked disparity, right-view disparity, valid mask), row-banded over the group."""
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        H, W = L.shape
+        out, rd, mask = (np.empty((H, W), np.uint8) for _ in range(3))
+        _capi.check(self._lib.sm_group_block_match_lr_u8(self._g, L.ctypes.data, R.ctypes.data, W, H, W, radius,
+                                                         num_disp, _flags(agg, True, median), out.ctypes.data,
+                                                         rd.ctypes.data, mask.ctypes.data, W))
+        return out, rd, mask
+
+    def match_batch(self, lefts, rights, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
+                    median: bool = False):
+        """A list of equal-size pairs; frame f runs on member f mod len(group)."""
+        Ls = [_as_u8_image(a, "left") for a in lefts]
+        Rs = [_as_u8_image(a, "right") for a in rights]
+        if len(Ls) != len(Rs) or any(a.shape != Ls[0].shape for a in Ls + Rs):
+            raise ValueError("expected equal-size left/right lists")
+        if not Ls:
+            return []
+        H, W = Ls[0].shape
+        outs = [np.empty((H, W), np.uint8) for _ in Ls]
+        n = len(Ls)
+        ptrs = lambda arrs: (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])  # noqa: E731
+        _capi.check(self._lib.sm_group_block_match_batch_u8(self._g, ptrs(Ls), ptrs(Rs), n, W, H, W, radius,
+                                                            num_disp, _flags(agg, lr_check, median), ptrs(outs), W))
+        return outs
 
 
 _default: Optional[BlockMatcher] = None

@@ -34,6 +34,8 @@ EXPORTED = (
     "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8", "sm_median_u8_device",
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
     "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
+    "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
+    "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8",
 )
 
 
@@ -91,6 +93,13 @@ def load(path: str = LIB_PATH):
     L.sm_stereo_rectify.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp]
     L.sm_init_rectify_map_device.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i, vp]
     L.sm_init_rectify_map.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i]
+    L.sm_create_group.argtypes = [i, vp, i, i, i, vp]
+    L.sm_destroy_group.argtypes = [vp]
+    L.sm_group_size.argtypes = [vp, vp]
+    L.sm_group_set_param_f.argtypes = [vp, i, ctypes.c_float]
+    L.sm_group_block_match_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, i]
+    L.sm_group_block_match_lr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, vp, vp, i]
+    L.sm_group_block_match_batch_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

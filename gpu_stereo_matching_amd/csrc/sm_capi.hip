@@ -10,8 +10,13 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <cstdarg>
+#include <functional>
+#include <mutex>
 #include <new>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sm_hip.h"
@@ -282,13 +287,27 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     return SM_OK;
 }
 
+// Host-pointer pass over one frame (or one row band of a frame: sm_group_*).  Only result rows
+// [keep0, keep1) are downloaded, into disp_out / right_out / mask_out pointing at row keep0.
+int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+                    int radius, int num_disp, unsigned flags, int keep0, int keep1, uint8_t* disp_out,
+                    uint8_t* right_out, uint8_t* mask_out, int out_pitch);
+
 int host_match(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
                int radius, int num_disp, unsigned flags, uint8_t* disp_out, uint8_t* right_out, uint8_t* mask_out,
                int out_pitch) {
+    return host_match_rows(h, left, right, width, height, pitch, radius, num_disp, flags, 0, height, disp_out,
+                           right_out, mask_out, out_pitch);
+}
+
+int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+                    int radius, int num_disp, unsigned flags, int keep0, int keep1, uint8_t* disp_out,
+                    uint8_t* right_out, uint8_t* mask_out, int out_pitch) {
     int rc = check_geometry(h, width, height, pitch, radius, num_disp);
     if (rc) return rc;
     if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
     if (out_pitch < width) return fail(SM_ERR_INVALID_ARG, "out_pitch %d < width %d", out_pitch, width);
+    if (keep0 < 0 || keep1 > height || keep0 >= keep1) return fail(SM_ERR_INVALID_ARG, "bad kept rows");
     if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
         return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity %dx%d/D=%d", width, height, num_disp,
                     h->max_w, h->max_h, h->max_d);
@@ -314,15 +333,126 @@ int host_match(sm_handle* h, const uint8_t* left, const uint8_t* right, int widt
                     right_out ? aux : nullptr, mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
     SM_HIP(hipEventRecord(h->ev[2], s));
-    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
-    if (right_out) SM_HIP(copy2d(right_out, out_pitch, aux, width, width, height, hipMemcpyDeviceToHost, s));
-    if (mask_out) SM_HIP(copy2d(mask_out, out_pitch, aux + P, width, width, height, hipMemcpyDeviceToHost, s));
+    const int64_t k0 = (int64_t)keep0 * width;
+    const int nk = keep1 - keep0;
+    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp + k0, width, width, nk, hipMemcpyDeviceToHost, s));
+    if (right_out) SM_HIP(copy2d(right_out, out_pitch, aux + k0, width, width, nk, hipMemcpyDeviceToHost, s));
+    if (mask_out) SM_HIP(copy2d(mask_out, out_pitch, aux + P + k0, width, width, nk, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
     SM_HIP(hipEventSynchronize(h->ev[3]));
     SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
     SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
     SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
     return SM_OK;
+}
+
+// ---- multi-GPU group (sm_create_group): one handle and one persistent host thread per device ----
+// Pageable host copies block their calling thread, so each device gets its own worker thread; a
+// call hands every worker its job (a row band of one frame, or a share of a frame batch) and
+// waits for all of them.
+struct GroupWorker {
+    sm_handle* h = nullptr;
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<int()> job;
+    bool has_job = false, done = false, quit = false;
+    int rc = SM_OK;
+    std::string err;
+
+    void loop() {
+        for (;;) {
+            std::function<int()> j;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return has_job || quit; });
+                if (quit) return;
+                j = std::move(job);
+                has_job = false;
+            }
+            const int r = j();
+            std::lock_guard<std::mutex> lk(m);
+            rc = r;
+            err = r ? std::string(g_err) : std::string();
+            done = true;
+            cv.notify_all();
+        }
+    }
+};
+
+}  // namespace
+
+struct sm_group {
+    std::vector<GroupWorker*> w;
+};
+
+namespace {
+
+// Runs jobs[k] on worker k (jobs may be shorter than the group: the rest stay idle) and returns the
+// first failure, its message re-raised on the calling thread.
+int group_run(sm_group* g, std::vector<std::function<int()>>& jobs) {
+    const size_t n = jobs.size() < g->w.size() ? jobs.size() : g->w.size();
+    for (size_t k = 0; k < n; ++k) {
+        GroupWorker* w = g->w[k];
+        std::lock_guard<std::mutex> lk(w->m);
+        w->job = std::move(jobs[k]);
+        w->has_job = true;
+        w->done = false;
+        w->cv.notify_all();
+    }
+    int rc = SM_OK;
+    std::string err;
+    for (size_t k = 0; k < n; ++k) {
+        GroupWorker* w = g->w[k];
+        std::unique_lock<std::mutex> lk(w->m);
+        w->cv.wait(lk, [&] { return w->done; });
+        if (w->rc && !rc) {
+            rc = w->rc;
+            err = "device " + std::to_string(w->h->device) + ": " + w->err;
+        }
+    }
+    if (rc) return fail(rc, "%s", err.c_str());
+    return SM_OK;
+}
+
+// Rows a band must see on each side of its output rows: the aggregation window (2r for the
+// guided filter's nested windows, at least 16 so that the guided kernel's 8-row float running
+// sums of the kept rows start on rows the band holds exactly) plus the median's 3.
+int group_halo(int radius, unsigned flags) {
+    int h = (flags & SM_AGG_GUIDED) ? (2 * radius > 16 ? 2 * radius : 16) : radius;
+    return h + ((flags & SM_MEDIAN) ? 3 : 0);
+}
+
+int group_bands(sm_group* g, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+                int radius, int num_disp, unsigned flags, uint8_t* disp_out, uint8_t* right_out, uint8_t* mask_out,
+                int out_pitch) {
+    if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
+    if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (width <= 0 || height <= 0 || pitch < width || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d pitch %d out_pitch %d", width, height, pitch,
+                    out_pitch);
+    // bands of whole 32-row tiles; each band's input starts on a 32-row boundary so that its tile
+    // grid is the full frame's (the kept rows are then bit-identical to a single-device pass)
+    constexpr int kAlign = 32;
+    const int n = (int)g->w.size();
+    const int tiles = (height + kAlign - 1) / kAlign;
+    const int per = ((tiles + n - 1) / n) * kAlign;
+    const int halo = group_halo(radius, flags);
+    std::vector<std::function<int()>> jobs;
+    for (int k = 0; k < n; ++k) {
+        const int y0 = k * per, y1 = (k + 1) * per < height ? (k + 1) * per : height;
+        if (y0 >= height) break;
+        const int a = y0 - halo <= 0 ? 0 : ((y0 - halo) / kAlign) * kAlign;
+        const int b = y1 + halo < height ? y1 + halo : height;
+        sm_handle* h = g->w[k]->h;
+        const int64_t ro = (int64_t)a * pitch, oo = (int64_t)y0 * out_pitch;
+        jobs.push_back([=]() -> int {
+            return host_match_rows(h, left + ro, right + ro, width, b - a, pitch, radius, num_disp, flags, y0 - a,
+                                   y1 - a, disp_out + oo, right_out ? right_out + oo : nullptr,
+                                   mask_out ? mask_out + oo : nullptr, out_pitch);
+        });
+    }
+    return group_run(g, jobs);
 }
 
 }  // namespace
@@ -739,6 +869,103 @@ SM_API int sm_stream_sync(sm_handle* h, void* stream) {
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(hipStreamSynchronize(stream ? (hipStream_t)stream : h->stream));
     return SM_OK;
+}
+
+
+SM_API int sm_create_group(int ngpu, const int* devices, int max_width, int max_height, int max_disp,
+                           sm_group** out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    if (ngpu < 1 || ngpu > 64) return fail(SM_ERR_INVALID_ARG, "group size %d out of [1, 64]", ngpu);
+    sm_group* g = new (std::nothrow) sm_group();
+    if (!g) return fail(SM_ERR_OUT_OF_MEMORY, "host alloc");
+    for (int k = 0; k < ngpu; ++k) {
+        sm_handle* h = nullptr;
+        const int rc = sm_create(devices ? devices[k] : k, max_width, max_height, max_disp, &h);
+        if (rc) {
+            const std::string msg = g_err;
+            sm_destroy_group(g);
+            return fail(rc, "group member %d: %s", k, msg.c_str());
+        }
+        GroupWorker* w = new (std::nothrow) GroupWorker();
+        if (!w) {
+            sm_destroy(h);
+            sm_destroy_group(g);
+            return fail(SM_ERR_OUT_OF_MEMORY, "host alloc");
+        }
+        w->h = h;
+        w->th = std::thread([w] { w->loop(); });
+        g->w.push_back(w);
+    }
+    *out = g;
+    return SM_OK;
+}
+
+SM_API int sm_destroy_group(sm_group* g) {
+    if (!g) return SM_OK;
+    for (GroupWorker* w : g->w) {
+        {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->quit = true;
+            w->cv.notify_all();
+        }
+        if (w->th.joinable()) w->th.join();
+        sm_destroy(w->h);
+        delete w;
+    }
+    delete g;
+    return SM_OK;
+}
+
+SM_API int sm_group_size(const sm_group* g, int* n) {
+    if (!g || !n) return fail(SM_ERR_INVALID_ARG, "null argument");
+    *n = (int)g->w.size();
+    return SM_OK;
+}
+
+SM_API int sm_group_set_param_f(sm_group* g, int param, float value) {
+    if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
+    for (GroupWorker* w : g->w) {
+        const int rc = sm_set_param_f(w->h, param, value);
+        if (rc) return rc;
+    }
+    return SM_OK;
+}
+
+SM_API int sm_group_block_match_u8(sm_group* g, const uint8_t* left, const uint8_t* right, int width, int height,
+                                   int pitch, int radius, int num_disp, unsigned flags, uint8_t* disp_out,
+                                   int out_pitch) {
+    return group_bands(g, left, right, width, height, pitch, radius, num_disp, flags, disp_out, nullptr, nullptr,
+                       out_pitch);
+}
+
+SM_API int sm_group_block_match_lr_u8(sm_group* g, const uint8_t* left, const uint8_t* right, int width, int height,
+                                      int pitch, int radius, int num_disp, unsigned flags, uint8_t* disp_out,
+                                      uint8_t* right_disp_out, uint8_t* valid_mask_out, int out_pitch) {
+    return group_bands(g, left, right, width, height, pitch, radius, num_disp, flags | SM_LR_CHECK, disp_out,
+                       right_disp_out, valid_mask_out, out_pitch);
+}
+
+SM_API int sm_group_block_match_batch_u8(sm_group* g, const uint8_t* const* lefts, const uint8_t* const* rights,
+                                         int nframes, int width, int height, int pitch, int radius, int num_disp,
+                                         unsigned flags, uint8_t* const* disps, int out_pitch) {
+    if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
+    if (nframes < 0 || (nframes > 0 && (!lefts || !rights || !disps)))
+        return fail(SM_ERR_INVALID_ARG, "bad frame arrays");
+    const int n = (int)g->w.size();
+    std::vector<std::function<int()>> jobs;
+    for (int k = 0; k < n && k < nframes; ++k) {
+        sm_handle* h = g->w[k]->h;
+        jobs.push_back([=]() -> int {
+            for (int f = k; f < nframes; f += n) {   // frame f on member f mod n, in order
+                const int rc = host_match(h, lefts[f], rights[f], width, height, pitch, radius, num_disp, flags,
+                                          disps[f], nullptr, nullptr, out_pitch);
+                if (rc) return rc;
+            }
+            return SM_OK;
+        });
+    }
+    return group_run(g, jobs);
 }
 
 }  // extern "C"

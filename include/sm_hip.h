@@ -188,6 +188,33 @@ SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const ui
                                  int width, int height, int pitch, int channels, int radius,
                                  int num_disp, unsigned flags, uint8_t *disp_out, int out_pitch);
 
+/* ---- several GPUs from one host thread (sm_create_group) ----
+ * A group holds one handle and one host worker thread per device (devices == NULL: 0..ngpu-1;
+ * a device may repeat).  Calls are synchronous, like sm_block_match_u8.
+ *  - sm_group_block_match[_lr]_u8: ONE frame in row bands of whole 32-row tiles, one band per
+ *    device, each matched from its rows plus the window halo (r; guided max(2r, 16); +3 with
+ *    SM_MEDIAN) and downloaded straight into its rows of disp_out.  Every flag is row-local, so
+ *    the result equals sm_block_match[_lr]_u8 bit for bit (the guided bands start on the full
+ *    frame's tile grid).  No device-to-device traffic: the host frame is the gather point.
+ *  - sm_group_block_match_batch_u8: nframes independent pairs, frame f on member f mod ngpu. */
+typedef struct sm_group sm_group;
+SM_API int sm_create_group(int ngpu, const int *devices, int max_width, int max_height, int max_disp,
+                           sm_group **out);
+SM_API int sm_destroy_group(sm_group *g);
+SM_API int sm_group_size(const sm_group *g, int *n);
+SM_API int sm_group_set_param_f(sm_group *g, int param, float value);
+SM_API int sm_group_block_match_u8(sm_group *g, const uint8_t *left, const uint8_t *right, int width,
+                                   int height, int pitch, int radius, int num_disp, unsigned flags,
+                                   uint8_t *disp_out, int out_pitch);
+SM_API int sm_group_block_match_lr_u8(sm_group *g, const uint8_t *left, const uint8_t *right, int width,
+                                      int height, int pitch, int radius, int num_disp, unsigned flags,
+                                      uint8_t *disp_out, uint8_t *right_disp_out, uint8_t *valid_mask_out,
+                                      int out_pitch);
+SM_API int sm_group_block_match_batch_u8(sm_group *g, const uint8_t *const *lefts,
+                                         const uint8_t *const *rights, int nframes, int width, int height,
+                                         int pitch, int radius, int num_disp, unsigned flags,
+                                         uint8_t *const *disps, int out_pitch);
+
 #ifdef __cplusplus
 }
 #endif

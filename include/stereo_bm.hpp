@@ -95,22 +95,47 @@ struct Size {                            // cv::Size: (width, height)
 
 namespace detail {
 
+// SM_DEVICE=k picks the device; SM_DEVICES=a,b,... (two or more) also builds a group handle
+// (sm_create_group) over those devices, and blockMatching_gpu / testBM / getDisp then split each
+// frame into row bands, one per device (bit-identical results).
 struct Engine {
     sm_handle* h = nullptr;
+    sm_group* g = nullptr;
     int w = 0, hgt = 0, d = 0;
-    ~Engine() { if (h) sm_destroy(h); }
+    ~Engine() {
+        if (g) sm_destroy_group(g);
+        if (h) sm_destroy(h);
+    }
+    static std::vector<int> device_list() {
+        std::vector<int> v;
+        if (const char* e = std::getenv("SM_DEVICES")) {
+            std::stringstream ss(e);
+            std::string tok;
+            while (std::getline(ss, tok, ','))
+                if (!tok.empty()) v.push_back(std::atoi(tok.c_str()));
+        }
+        return v;
+    }
     bool ensure(int width, int height, int ndisp) {
         if (h && width <= w && height <= hgt && ndisp <= d) return true;
+        if (g) sm_destroy_group(g);
         if (h) sm_destroy(h);
         h = nullptr;
+        g = nullptr;
         w = width > 1920 ? width : 1920;
         hgt = height > 1080 ? height : 1080;
         d = 256;
-        int dev = 0;
+        const std::vector<int> devs = device_list();
+        int dev = devs.empty() ? 0 : devs[0];
         if (const char* e = std::getenv("SM_DEVICE")) dev = std::atoi(e);
         if (sm_create(dev, w, hgt, d, &h) != SM_OK) {
             std::cerr << "sm_create: " << sm_last_error_string() << std::endl;
             h = nullptr;
+            return false;
+        }
+        if (devs.size() > 1 && sm_create_group((int)devs.size(), devs.data(), w, hgt, d, &g) != SM_OK) {
+            std::cerr << "sm_create_group: " << sm_last_error_string() << std::endl;
+            g = nullptr;
             return false;
         }
         return true;
@@ -140,15 +165,18 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     }
     detail::Engine& e = detail::engine();
     if (!e.ensure(cols, rows, searchRange)) return SM_ERR_DEVICE;
-    int rc = sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
-                               SADWindowSize, searchRange, flags, h_disparity.data,
-                               (int)detail::row_step(h_disparity));
+    int rc = e.g ? sm_group_block_match_u8(e.g, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
+                                           SADWindowSize, searchRange, flags, h_disparity.data,
+                                           (int)detail::row_step(h_disparity))
+                 : sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
+                                     SADWindowSize, searchRange, flags, h_disparity.data,
+                                     (int)detail::row_step(h_disparity));
     if (rc != SM_OK) {
         std::cerr << "blockMatching_gpu: " << sm_last_error_string() << std::endl;
         for (int r = 0; r < rows; ++r) std::memset(h_disparity.data + (size_t)r * detail::row_step(h_disparity), 0, cols);
         return rc;
     }
-    if (std::getenv("SM_VERBOSE")) {
+    if (std::getenv("SM_VERBOSE") && !e.g) {
         float up = 0, mt = 0, dn = 0;
         sm_last_stage_ms(e.h, &up, &mt, &dn);
         std::cout << "upload data : " << up << std::endl;        // Device.cu:218
@@ -215,8 +243,11 @@ inline void testBM(const SmHostMat& left0, const SmHostMat& right0, SmHostMat& d
 inline void getDisp(const SmHostMat& left0, const SmHostMat& right0, uchar* disparity, int SAD, int searchRange) {
     sm::detail::Engine& e = sm::detail::engine();
     if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
-    if (sm_block_match_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, (int)sm::detail::row_step(left0),
-                          SAD, searchRange, SM_AGG_BOX, disparity, left0.cols) != SM_OK)
+    const int lp = (int)sm::detail::row_step(left0);
+    if ((e.g ? sm_group_block_match_u8(e.g, left0.data, right0.data, left0.cols, left0.rows, lp, SAD, searchRange,
+                                       SM_AGG_BOX, disparity, left0.cols)
+             : sm_block_match_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, lp, SAD, searchRange,
+                                 SM_AGG_BOX, disparity, left0.cols)) != SM_OK)
         std::cerr << "getDisp: " << sm_last_error_string() << std::endl;
 }
 // PreCal (BlockMatching.cpp:89-109): the AD volume, searchRange d-major planes of rows*cols bytes.

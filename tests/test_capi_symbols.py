@@ -41,6 +41,25 @@ def test_version_and_errors_without_device():
         assert lib.sm_create(0, 64, 64, 64, ctypes.byref(h)) == _capi.SM_ERR_DEVICE
 
 
+def test_group_errors_without_device():
+    """The multi-GPU group handle: argument checks, and member creation failing cleanly (the
+    partially built group is torn down, its worker threads joined) when no device is visible."""
+    from gpu_stereo_matching_amd import _capi
+    lib = _capi.load()
+    g = ctypes.c_void_p()
+    assert lib.sm_create_group(0, None, 64, 64, 64, ctypes.byref(g)) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_create_group(2, None, 64, 64, 64, None) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_group_block_match_u8(None, None, None, 8, 8, 8, 1, 8, 0, None, 8) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_group_block_match_batch_u8(None, None, None, 1, 8, 8, 8, 1, 8, 0, None, 8) == _capi.SM_ERR_INVALID_ARG
+    assert lib.sm_destroy_group(None) == _capi.SM_OK
+    n = ctypes.c_int(-1)
+    lib.sm_device_count(ctypes.byref(n))
+    if n.value == 0:
+        assert lib.sm_create_group(2, None, 64, 64, 64, ctypes.byref(g)) == _capi.SM_ERR_DEVICE
+        assert b"group member 0" in lib.sm_last_error_string()
+        assert not g.value
+
+
 def test_no_cpu_fallback_in_product():
     """The product package must not import or load the oracle (test infrastructure only)."""
     pkg = os.path.join(ROOT, "gpu_stereo_matching_amd")

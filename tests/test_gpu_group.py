@@ -1,0 +1,74 @@
+"""The multi-GPU group handle of the C ABI (sm_create_group) on the one GPU of the test box: a
+group may name a device more than once, so 2-3 members on device 0 exercise the banding, the
+per-member worker threads and the batch split exactly as distinct GPUs would.  Row-banded results
+must equal the single-handle pass bit for bit (every flag is row-local; guided bands start on the
+full frame's tile grid), including the guided filter's float path."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EPS = 1e-4 * 255 * 255
+
+
+@pytest.fixture(scope="module")
+def single():
+    import gpu_stereo_matching_amd as sm
+    m = sm.BlockMatcher(0, 1920, 1080, 256)
+    m.set_guided_eps(EPS)
+    yield m
+    m.close()
+
+
+def _pair(W, H, D, seed=99):
+    from oracle import oracle as O
+    return O.synth_pair(seed, W, H, max(D, 16))
+
+
+@pytest.mark.parametrize("members", [2, 3])
+@pytest.mark.parametrize("agg,lr,med,r,D", [("box", False, False, 5, 128), ("box", True, False, 4, 64),
+                                            ("box", True, True, 3, 64), ("guided", False, False, 5, 64),
+                                            ("guided", True, False, 7, 48), ("box-staged", False, False, 5, 64)])
+def test_group_row_bands_bit_exact(single, members, agg, lr, med, r, D):
+    import gpu_stereo_matching_amd as sm
+    W, H = 640, 333
+    L, R = _pair(W, H, D)
+    with sm.BlockMatcherGroup([0] * members, 1920, 1080, 256) as g:
+        assert len(g) == members
+        g.set_guided_eps(EPS)
+        if lr:
+            got = g.match_lr(L, R, r, D, agg=agg, median=med)
+            want = single.match_lr(L, R, r, D, agg=agg, median=med)
+            for a, b in zip(got, want):
+                assert np.array_equal(a, b)
+        else:
+            assert np.array_equal(g.match(L, R, r, D, agg=agg, median=med), single.match(L, R, r, D, agg=agg,
+                                                                                         median=med))
+
+
+def test_group_more_members_than_tiles(single):
+    """A frame with fewer 32-row tiles than members: the extra members stay idle."""
+    import gpu_stereo_matching_amd as sm
+    L, R = _pair(200, 40, 32)
+    with sm.BlockMatcherGroup([0, 0, 0], 512, 256, 64) as g:
+        assert np.array_equal(g.match(L, R, 2, 32), single.match(L, R, 2, 32))
+
+
+def test_group_batch(single):
+    import gpu_stereo_matching_amd as sm
+    pairs = [_pair(320, 120, 64, seed=s) for s in range(5)]
+    with sm.BlockMatcherGroup([0, 0], 512, 256, 64) as g:
+        outs = g.match_batch([p[0] for p in pairs], [p[1] for p in pairs], 4, 64, lr_check=True)
+    for (L, R), o in zip(pairs, outs):
+        assert np.array_equal(o, single.match(L, R, 4, 64, lr_check=True))
+
+
+def test_group_error_from_a_member():
+    """A member's failure comes back on the calling thread with its message."""
+    import gpu_stereo_matching_amd as sm
+    from gpu_stereo_matching_amd import _capi
+    L, R = _pair(300, 64, 16)
+    with sm.BlockMatcherGroup([0, 0], 256, 64, 64) as g:          # capacity 256 wide < 300
+        with pytest.raises(_capi.SMError) as e:
+            g.match(L, R, 2, 16)
+    assert e.value.code == _capi.SM_ERR_CAPACITY and "device 0" in str(e.value)
