@@ -387,6 +387,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
 // partial rows cover u (x0 - DMAX - 1 <= u < x0 + TW, x0 <= u + d_hi - 1); dR = key & 0xFF with no
 // threshold (StereoHelper.cpp:131-154).  Then StereoDisparity.cpp:136-147 on the row:
 //   d = dL(x); occ = x-d < 0 || d == 0 || |d - dR(x-d)| > 1;  out = occ ? 0 : d.
+template <int MAXT>
 __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
                                                               int tiles_y, int TW, int PW, int dmax, int d_hi, int W,
                                                               int H, int check, uint8_t* disp, int opitch, int64_t ostride,
@@ -402,8 +403,13 @@ __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __
     for (int u = threadIdx.x; u < W; u += blockDim.x) {
         const int tlo = u / TW;
         const int thi = min(tiles_x - 1, (u + d_hi - 1) / TW);
+        // at most MAXT tiles cover u: fixed trip count, so all the loads issue before the first use
         uint32_t key = 0xFFFFFFFFu;
-        for (int tx = tlo; tx <= thi; ++tx) key = min(key, base[tx * tstride + (u - tx * TW + dmax + 1)]);
+#pragma unroll
+        for (int k = 0; k < MAXT; ++k) {
+            const int tx = tlo + k;
+            if (tx <= thi) key = min(key, base[tx * tstride + (u - tx * TW + dmax + 1)]);
+        }
         const uint8_t dr = (uint8_t)(key & 0xFFu);
         dr_row[u] = dr;
         if (rrow) rrow[u] = dr;
@@ -445,8 +451,10 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
                            (size_t)G::LDS_BYTES_R, s, a, tiles_x, tiles_y);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(right_reduce_lr_kernel, dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart, tiles_x,
-                           tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
+        // tiles covering one u: (TW + d_hi - 1) / TW + 1 at most
+        constexpr int kMaxT = (G::TW + DMAX - 1) / G::TW + 1;
+        hipLaunchKernelGGL((right_reduce_lr_kernel<kMaxT>), dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart,
+                           tiles_x, tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
                            a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
     } else {
         hipLaunchKernelGGL((box_match_kernel<R, DMAX, false>), dim3((unsigned)blocks), dim3(64 * kWaves<false, R>),
