@@ -510,6 +510,95 @@ done:
 }
 
 /* ------------------------------------------------------------------------- */
+/* The same fp64 guided filter, probed at given disparities in O(P) memory    */
+/* (full-size checks, cfg3 at 1920x1080 D=128, without the D x P volume):     */
+/*   left : best[p] / bd[p] as ora_guided_disp; qL[p] = q(p, dL[p]) (x+d<=W   */
+/*          or not: the raw cost);                                           */
+/*   right: STMatching's C_R(y,u,d) = q(y,u+d,d) if u+d < W, else C_R(u,d-1) */
+/*          (StereoHelper.cpp:156-180); bestR[u] = min_d C_R, qR[u] =        */
+/*          C_R(u, dR[u]).  dR / the right outputs may be NULL.              */
+/* ------------------------------------------------------------------------- */
+ORA_API int ora_guided_probe(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D, double eps,
+                             const uint8_t *dL, const uint8_t *dR, uint8_t *out, double *best_out, double *qL,
+                             double *bestR, double *qR)
+{
+    const int64_t P = (int64_t)W * H;
+    int64_t *isrc = (int64_t *)malloc(sizeof(int64_t) * P);
+    int64_t *itmp = (int64_t *)malloc(sizeof(int64_t) * P);
+    double *mI = (double *)malloc(sizeof(double) * P);
+    double *mII = (double *)malloc(sizeof(double) * P);
+    double *mp = (double *)malloc(sizeof(double) * P);
+    double *mIp = (double *)malloc(sizeof(double) * P);
+    double *a = (double *)malloc(sizeof(double) * P);
+    double *b = (double *)malloc(sizeof(double) * P);
+    double *ma = (double *)malloc(sizeof(double) * P);
+    double *mb = (double *)malloc(sizeof(double) * P);
+    double *dtmp = (double *)malloc(sizeof(double) * P);
+    double *best = (double *)malloc(sizeof(double) * P);
+    int *bd = (int *)malloc(sizeof(int) * P);
+    int rc = 0;
+    if (!isrc || !itmp || !mI || !mII || !mp || !mIp || !a || !b || !ma || !mb || !dtmp || !best || !bd) {
+        rc = -1;
+        goto done;
+    }
+    for (int64_t p = 0; p < P; ++p) isrc[p] = L[p];
+    box_mean_i(isrc, W, H, radius, itmp, mI);
+    for (int64_t p = 0; p < P; ++p) isrc[p] = (int64_t)L[p] * L[p];
+    box_mean_i(isrc, W, H, radius, itmp, mII);
+    for (int64_t p = 0; p < P; ++p) {
+        best[p] = 50.0;
+        bd[p] = -256;
+        if (bestR) bestR[p] = 1e300;
+    }
+    for (int d = 0; d < D; ++d) {
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                int64_t p = (int64_t)y * W + x;
+                int v = 0;
+                if (x >= d) { v = (int)L[p] - (int)R[p - d]; if (v < 0) v = -v; }
+                isrc[p] = v;
+            }
+        box_mean_i(isrc, W, H, radius, itmp, mp);
+        for (int64_t p = 0; p < P; ++p) isrc[p] *= L[p];
+        box_mean_i(isrc, W, H, radius, itmp, mIp);
+        for (int64_t p = 0; p < P; ++p) {
+            double var = mII[p] - mI[p] * mI[p];
+            double cov = mIp[p] - mI[p] * mp[p];
+            a[p] = cov / (var + eps);
+            b[p] = mp[p] - a[p] * mI[p];
+        }
+        box_mean_d(a, W, H, radius, dtmp, ma);
+        box_mean_d(b, W, H, radius, dtmp, mb);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                int64_t p = (int64_t)y * W + x;
+                double q = ma[p] * (double)L[p] + mb[p];
+                if (qL && dL && dL[p] == d) qL[p] = q;
+                /* right pixel u = x - d sees q as C_R(u, d); u + d < W holds (x < W) */
+                int u = x - d;
+                if (u >= 0 && bestR) {
+                    int64_t pu = (int64_t)y * W + u;
+                    if (q < bestR[pu]) bestR[pu] = q;
+                    if (qR && dR) {
+                        int dr = dR[pu], lim = W - 1 - u;   /* C_R(u, dr) = C_R(u, min(dr, lim)) */
+                        if ((dr <= lim ? dr : lim) == d) qR[pu] = q;
+                    }
+                }
+                if (x + d > W) continue;
+                if (q < best[p]) { best[p] = q; bd[p] = d; }
+            }
+    }
+    for (int64_t p = 0; p < P; ++p) {
+        if (out) out[p] = (uint8_t)bd[p];
+        if (best_out) best_out[p] = best[p];
+    }
+done:
+    free(isrc); free(itmp); free(mI); free(mII); free(mp); free(mIp); free(a); free(b);
+    free(ma); free(mb); free(dtmp); free(best); free(bd);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic rectified pair: SplitMix64(seed) texture T of      */
 /* H x (W + 2D); L[y][x] = T[y][x + D], R[y][x] = T[y][x + D + gt(y)],       */
 /* gt(y) = 8 + floor(8y/H) * floor((D-16)/7) (clamped at >= 0 bands).         */

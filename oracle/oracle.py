@@ -61,6 +61,9 @@ def lib():
         L.ora_init_rectify_map.argtypes = [_f64p, _f64p, ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.ora_synth_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
+        L.ora_guided_probe.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_double, _u8p, _u8p, _u8p, _f64p, _f64p, _f64p, _f64p]
+        L.ora_guided_probe.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -161,6 +164,26 @@ def box_lr(left, right, radius: int, D: int):
     rdisp = right_wta(cost)
     checked, mask = lr_check(disp, rdisp)
     return disp, rdisp, checked, mask
+
+
+def guided_probe(left, right, radius: int, D: int, eps: float, disp_left, disp_right=None):
+    """The fp64 guided filter probed at given maps in O(P) memory (full-size checks):
+    (oracle disparity, best left cost, left cost at disp_left, best right cost, right cost at
+    disp_right); the right costs follow StereoHelper.cpp:156-180 (None without disp_right)."""
+    left, right = _img(left), _img(right)
+    H, W = left.shape
+    dl = _img(disp_left)
+    dr = _img(disp_right) if disp_right is not None else None
+    out = np.empty((H, W), np.uint8)
+    best, qL = np.empty((H, W), np.float64), np.empty((H, W), np.float64)
+    bestR = np.empty((H, W), np.float64) if dr is not None else None
+    qR = np.empty((H, W), np.float64) if dr is not None else None
+    rc = lib().ora_guided_probe(_p(left, _u8p), _p(right, _u8p), W, H, radius, D, float(eps), _p(dl, _u8p),
+                                _p(dr, _u8p), _p(out, _u8p), _p(best, _f64p), _p(qL, _f64p), _p(bestR, _f64p),
+                                _p(qR, _f64p))
+    if rc != 0:
+        raise MemoryError("ora_guided_probe")
+    return out, best, qL, bestR, qR
 
 
 def right_cost_from_left(cost: np.ndarray) -> np.ndarray:

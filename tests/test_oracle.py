@@ -156,3 +156,18 @@ def test_right_wta_float_matches_int_restatement(oracle, gray):
     u = W - 5                                    # clamp rule: C_R(u, d) = C_R(u, d-1) for u + d >= W
     assert np.array_equal(cr[10:, :, u], np.repeat(cr[4:5, :, u], 38, axis=0))
     assert np.array_equal(best, cr.min(axis=0))
+
+
+def test_guided_probe_matches_volume_oracle(oracle):
+    """The O(P) probe (full-size guided checks) == the volume restatement: best, the left cost at a
+    map, and the right-view costs of StereoHelper.cpp:156-180 including the u + d >= W clamp."""
+    L, R = oracle.synth_pair(5, 90, 40, 32)
+    eps = 1e-4 * 255 * 255
+    disp, q, best = oracle.guided_disp(L, R, 3, 32, eps, want_q=True)
+    rd, cr, bestr = oracle.right_wta_float(q)
+    probe_r = np.random.default_rng(0).integers(0, 32, L.shape).astype(np.uint8)
+    out, b2, qL, bR, qR = oracle.guided_probe(L, R, 3, 32, eps, disp, probe_r)
+    ys, xs = np.mgrid[0:40, 0:90]
+    assert np.array_equal(out, disp) and np.array_equal(b2, best) and np.array_equal(bR, bestr)
+    assert np.array_equal(qL, q[disp.astype(int), ys, xs])
+    assert np.array_equal(qR, cr[probe_r.astype(int), ys, xs])
