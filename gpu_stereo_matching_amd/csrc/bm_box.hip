@@ -468,13 +468,16 @@ hipError_t launch_r(const MatchArgs& a, int batch, const RightOut* ro, hipStream
     const int dspan = (a.d_hi - a.d_lo + kChunk - 1) & ~(kChunk - 1);
     if (dspan <= 64) return launch_rd<R, 64, RIGHT>(a, batch, ro, s);
     if (dspan <= 128) return launch_rd<R, 128, RIGHT>(a, batch, ro, s);
+    // 192 (cfg5): the right band and the right-key rows sized for 192, not 256, keep the plain kernel
+    // at 4 workgroups/CU and the right-view kernel at 2
+    if (dspan <= 192) return launch_rd<R, 192, RIGHT>(a, batch, ro, s);
     return launch_rd<R, 256, RIGHT>(a, batch, ro, s);
 }
 
 template <int R>
 size_t partial_bytes_r(int W, int H, int D, int batch) {
     const int dspan = (D + kChunk - 1) & ~(kChunk - 1);
-    const int dmax = dspan <= 64 ? 64 : (dspan <= 128 ? 128 : 256);
+    const int dmax = dspan <= 64 ? 64 : (dspan <= 128 ? 128 : (dspan <= 192 ? 192 : 256));
     const int TW = kCols - 2 * R;
     const int PW = TW + dmax + 1;
     const size_t tiles = (size_t)((W + TW - 1) / TW) * ((H + kTileH - 1) / kTileH);
