@@ -326,6 +326,50 @@ def test_frame_stream_consume_callback(matcher, oracle):
             assert np.array_equal(got[i], oracle.box_disp(Ls[i], Rs[i], r, D))
 
 
+@pytest.mark.parametrize("mode", ["bgr", "rectify", "bgr+rectify"])
+def test_frame_stream_camera_chain(matcher, oracle, mode):
+    """FrameStream with the front end on the GPU: BGR frames -> gray (Caller.cpp:15-16) and/or the
+    calibration's rectification maps (Rectify + remap, Caller.cpp:27-74) -> match; every batch
+    equals the oracle chain (bgr_to_gray -> remap -> box_disp) bit for bit."""
+    import os
+    from gpu_stereo_matching_amd import calib
+    from gpu_stereo_matching_amd.pipeline import FrameStream
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    chess = np.load(os.path.join(golden, "chess_set2_gray.npz"))
+    Lg, Rg = chess["Left_320x200"], chess["Right_320x200"]
+    H, W = Lg.shape
+    B, r, D = 2, 4, 48
+    rng = np.random.default_rng(5)
+    # BGR frames whose OpenCV gray is known: random colour, then the oracle's conversion
+    Lb = [rng.integers(0, 256, (H, W, 3), dtype=np.uint8) for _ in range(B)]
+    Rb = [np.roll(x, -7, axis=1) for x in Lb]
+    maps = None
+    if "rectify" in mode:
+        K1, K2, d1, d2, Rm, T = calib.load_data_batch(os.path.join(golden, "Calib_Data_OpenCV.yml"))
+        R1, R2, P1, P2, _ = calib.stereo_rectify(K1, d1, K2, d2, (W, H), Rm, T)
+        maps = (*oracle.init_rectify_map(K1, d1, R1, P1, W, H), *oracle.init_rectify_map(K2, d2, R2, P2, W, H))
+    if "bgr" in mode:
+        lefts, rights = np.stack(Lb), np.stack(Rb)
+        gl = [oracle.bgr_to_gray(x) for x in Lb]
+        gr = [oracle.bgr_to_gray(x) for x in Rb]
+    else:
+        lefts, rights = np.stack([Lg, Lg[::-1].copy()]), np.stack([Rg, Rg[::-1].copy()])
+        gl, gr = list(lefts), list(rights)
+    if maps is not None:
+        gl = [oracle.remap(g, maps[0], maps[1]) for g in gl]
+        gr = [oracle.remap(g, maps[2], maps[3]) for g in gr]
+    want = [oracle.box_disp(a, b, r, D) for a, b in zip(gl, gr)]
+    fs = FrameStream(matcher, B, W, H, r, D, bgr="bgr" in mode, rectify_maps=maps)
+    outs = []
+    for _ in range(3):
+        outs += fs.submit(lefts, rights)
+    outs += fs.flush()
+    assert len(outs) == 3
+    for got in outs:
+        for i in range(B):
+            assert np.array_equal(got[i], want[i])
+
+
 @pytest.mark.parametrize("W,H,D", [(64, 16, 8), (333, 77, 100), (1920, 1080, 128), (5, 3, 7)])
 def test_ad_volume(matcher, oracle, torch, W, H, D):
     """PreCal / kernalPreCal_V2 (row a1) as a standalone HBM-bound kernel, bit-exact."""
