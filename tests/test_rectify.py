@@ -232,3 +232,44 @@ def test_gpu_remap_test_chain(oracle, calib_data, chess, key):
             got = m.remap(img, mx, my)
             assert np.array_equal(got, oracle.remap(img, mx, my))
             assert (got > 0).mean() > 0.5      # the rectified view is mostly inside the source
+
+
+def test_cpp_adapter_load_data_batch(tmp_path):
+    """sm::LoadDataBatch / sm::LoadData in include/stereo_bm.hpp (Utility.cpp:17-42) parse the
+    reference's calibration YAML to the same CV_64FC1 values as the Python loader.  Host-only: the
+    parser calls nothing in the library, so the test program needs no GPU and no link."""
+    import subprocess
+    from gpu_stereo_matching_amd import calib
+    from conftest import ROOT
+    src = tmp_path / "ldb.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include "stereo_bm.hpp"
+int main(int argc, char** argv) {
+    sm::Mat m[6];
+    if (!sm::LoadDataBatch(argv[1], m[0], m[1], m[2], m[3], m[4], m[5])) return 2;
+    for (auto& a : m) {
+        std::printf("%d %d", a.rows, a.cols);
+        for (int r = 0; r < a.rows; ++r)
+            for (int c = 0; c < a.cols; ++c) std::printf(" %.17g", a.ptr<double>(r)[c]);
+        std::printf("\n");
+    }
+    sm::Mat t = sm::LoadData(argv[1], "TranslationVec");
+    std::printf("%d %d %.17g\n", t.rows, t.cols, t.ptr<double>(0)[0]);
+    sm::Mat none;
+    return sm::LoadDataBatch(argv[1] + std::string(".missing"), none, none, none, none, none, none) ? 3 : 0;
+}
+''')
+    exe = tmp_path / "ldb"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    r = subprocess.run([str(exe), YML], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    want = calib.load_data_batch(YML)
+    for line, w in zip(lines[:6], want):
+        vals = line.split()
+        assert (int(vals[0]), int(vals[1])) == w.shape
+        assert np.array_equal(np.array([float(v) for v in vals[2:]]).reshape(w.shape), w)
+    assert lines[6].split()[:2] == ["3", "1"] and float(lines[6].split()[2]) == want[5][0, 0]
+    assert "cannot open" in r.stderr
