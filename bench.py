@@ -395,7 +395,9 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"cfg3: {W}x{H} synthetic rectified pairs, {2*r+1}x{2*r+1} SAD box aggregation + WTA "
-                            f"(bit-exact with getDisp/kernalFindCorr), d_max={D}",
+                            f"(bit-exact with getDisp/kernalFindCorr), d_max={D}; the path BASELINE.md's GPU-target "
+                            f"table and the north star's >=100x CPU BlockMatching.cpp target are quoted on; "
+                            f"BASELINE configs[2]'s guided-filter aggregation of the same frames: 'cfg3_guided'",
                 "width": W, "height": H, "num_disp": D, "radius": r, "frames_per_step_per_gpu": B,
                 "seed": args.seed, "parallelism": f"frame-parallel x{world}",
             },
@@ -417,6 +419,17 @@ def main():
             res["rowband"] = rowband
         if variants:
             res["variants"] = variants
+            # BASELINE configs[2] as written (11x11 + guided-filter aggregation, 1080p d_max=128),
+            # the same synthetic frames, 4 per launch; no CPU port of the guided path is timed here
+            # (the fp64 oracle takes ~17 s per 1080p map on one core: tests/test_gpu_guided.py)
+            g = variants.get("cfg3 1080p 11x11 guided d128", {})
+            glr = variants.get("cfg3 1080p 11x11 guided+lr d128", {})
+            if "maps_per_s" in g:
+                res["cfg3_guided"] = {"value": g["maps_per_s"], "unit": "disparity-maps/s",
+                                      "ms_per_frame": g["ms_per_frame"], "frames_per_step": g["frames_per_call"],
+                                      "with_lr_check": {"value": glr.get("maps_per_s"),
+                                                        "ms_per_frame": glr.get("ms_per_frame")},
+                                      "kernel": "guided_fused_kernel<5>", "dtype": "fp32 (u8 in/out)"}
         print(json.dumps(res), flush=True)
 
     m.close()
