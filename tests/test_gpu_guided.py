@@ -120,3 +120,23 @@ def test_guided_lr_full_cfg3(matcher, oracle):
     assert ok_r.all(), f"right: {int((~ok_r).sum())} pixels outside the tie-aware tolerance"
     chk_o, mask_o = oracle.lr_check(left, rd)
     assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+
+
+def test_guided_lr_batched_device_and_median(matcher, oracle):
+    """Batched device calls of the fused guided right view (per-frame right-key partials) give each
+    frame's single-call result; with SM_MEDIAN both maps are filtered before the check."""
+    import torch
+    W, H, D, r = 300, 70, 64, 4
+    pairs = [oracle.synth_pair(40 + i, W, H, D) for i in range(3)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    for med in (False, True):
+        out = matcher.match_device(Lt, Rt, r, D, agg="guided", lr_check=True, median=med)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for i, (L, R) in enumerate(pairs):
+            chk, rd, mask = matcher.match_lr(L, R, r, D, agg="guided", median=med)
+            assert np.array_equal(got[i], chk)
+        if med:
+            left = matcher.match(L, R, r, D, agg="guided", median=True)
+            assert np.array_equal(chk, oracle.lr_check(left, rd)[0])
