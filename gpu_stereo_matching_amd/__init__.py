@@ -296,6 +296,29 @@ class BlockMatcher:
                                                      self._stream_ptr(stream)))
         return out_t
 
+    def guided_slice_keys_device(self, left_t, right_t, radius: int, d_lo: int, d_hi: int, keys_t=None,
+                                 stream=None):
+        """Guided-aggregation d-slice keys ((int32)(q * 2^14) << 8 | d, INT32_MAX where no d of the slice
+        is valid) as an int32 [H, W] tensor; disjoint slices combine with a signed elementwise min."""
+        import torch
+        H, W = left_t.shape[-2:]
+        if keys_t is None:
+            keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        _capi.check(self._lib.sm_guided_slice_keys_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W,
+                                                          radius, d_lo, d_hi, keys_t.data_ptr(),
+                                                          self._stream_ptr(stream)))
+        return keys_t
+
+    def guided_keys_to_disp_device(self, keys_t, out_t=None, stream=None):
+        """Combined guided keys -> uint8 disparity (d where q < 50, else 0)."""
+        import torch
+        H, W = keys_t.shape[-2:]
+        if out_t is None:
+            out_t = torch.empty((H, W), dtype=torch.uint8, device=keys_t.device)
+        _capi.check(self._lib.sm_guided_keys_to_disp_device(self._h, keys_t.data_ptr(), W, H, out_t.data_ptr(), W,
+                                                            self._stream_ptr(stream)))
+        return out_t
+
 
 class BlockMatcherGroup:
     """Several GPUs driven from this process through the C ABI's group handle (``sm_create_group``):

@@ -35,7 +35,8 @@ EXPORTED = (
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
     "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
-    "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8",
+    "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_guided_slice_keys_device",
+    "sm_guided_keys_to_disp_device",
 )
 
 
@@ -80,6 +81,8 @@ def load(path: str = LIB_PATH):
     L.sm_match_device.argtypes = [vp, vp, vp, i, i, i, i, i64, i, i, u, vp, i, i64, vp]
     L.sm_slice_keys_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp, vp]
     L.sm_keys_to_disp_device.argtypes = [vp, vp, i, i, i, vp, i, vp]
+    L.sm_guided_slice_keys_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp, vp]
+    L.sm_guided_keys_to_disp_device.argtypes = [vp, vp, i, i, vp, i, vp]
     L.sm_stream_sync.argtypes = [vp, vp]
     L.sm_median_u8_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
     L.sm_bgr_to_gray_u8.argtypes = [vp, vp, i, i, i, i, vp, i]

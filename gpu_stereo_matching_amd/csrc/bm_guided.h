@@ -22,4 +22,13 @@ hipError_t launch_guided_match_lr(const uint8_t* L, const uint8_t* R, int W, int
                                   int64_t rstride, hipStream_t s);
 size_t guided_right_partial_bytes(int W, int H, int radius, int D, int batch);
 
+// d-slice keys of the guided path (multi-GPU sharding over d): per pixel of each frame
+// ([batch][H][W] int32), ((int)(q * 2^14) << 8) | d for the best d in [d_lo, d_hi) (valid d <= W - x,
+// no threshold), INT_MAX if none is valid.  Keys of disjoint slices combine with a signed min.
+hipError_t launch_guided_slice_keys(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                    int64_t frame_stride, int radius, int d_lo, int d_hi, float eps, int* keys,
+                                    hipStream_t s);
+// combined keys -> disparity with the Device.cu:37 threshold q < 50
+hipError_t launch_guided_keys_to_disp(const int* keys, int W, int H, uint8_t* disp, int out_pitch, hipStream_t s);
+
 }  // namespace sm

@@ -129,8 +129,8 @@ constexpr float kRightMin = -8388608.0f;   // -2^23
 template <int R, bool RIGHT>
 __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
-    int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride, int tiles_x,
-    int tiles, int* __restrict__ gpart, int K) {
+    int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
+    int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
     using G = GeoF<R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = ld4(Rf, py0 + i, rbase + 4 * j, W, H, pitch);
         }
     };
-    stage_band(0);
+    stage_band(d_lo / kBandChunk);
     for (int e = tid; e < G::PHP * 16; e += kT) {
         const int i = e >> 4, j = e & 15;
         *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = ld4(L, py0 + i, px0 + 4 * j, W, H, pitch);
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         oI[o] = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
-        dlim[o] = valid_mode == 0 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
+        dlim[o] = valid_mode != 1 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
         if constexpr (RIGHT) {
             rinv[o] = ok ? kRightScale / (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_nanf("");
             rk[o] = INT_MAX;
@@ -398,23 +398,23 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
 
     s1v(0, std::true_type{}, std::false_type{});
     const bool s1_nomask = px0 >= D - 1 && px0 >= 0 && px0 + 63 < W;
-    const bool s2_lim = valid_mode == 0 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
+    const bool s2_lim = valid_mode != 1 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
     __syncthreads();
     s1h_stats();
     __syncthreads();
     // buffers: cs (S1V -> S1H), abp (S1H -> S2V), mm (S2V -> S2H); each producer of iteration d+1
     // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
     // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
-    for (int d = 0; d <= D; ++d) {
+    for (int d = d_lo; d <= D; ++d) {
         if (d < D) {
             if (s1_nomask) s1v(d, std::false_type{}, std::true_type{});
             else s1v(d, std::false_type{}, std::false_type{});
         }
-        if (d > 0) s2v();
+        if (d > d_lo) s2v();
         __syncthreads();
         if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
         if (d < D) s1h();
-        if (d > 0) {
+        if (d > d_lo) {
             if (s2_lim) s2h(d - 1, std::true_type{});
             else s2h(d - 1, std::false_type{});
         }
@@ -424,6 +424,20 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     if constexpr (RIGHT) {
         for (int k = D; k < K; ++k) chain_step(k);
     }
+    if (valid_mode == 2) {
+        // d-slice keys: (q * 2^14 << 8) | d, INT_MAX where no d of the slice is valid
+        int* Kf = keys + (int64_t)frame * H * W;
+#pragma unroll
+        for (int o = 0; o < G::SW2; ++o) {
+            const int x = x0 + h2s * G::SW2 + o;
+            if (oy < H && x < W && h2s * G::SW2 + o < G::TW) {
+                const float s = kRightScale / (float)(win_count(x, R, W) * win_count(oy, R, H));
+                const float qs = __builtin_fmaxf(__builtin_fminf(bq[o] * s, kRightMax), kRightMin);
+                Kf[(int64_t)oy * W + x] = bdd[o] < 0 ? INT_MAX : (((int)qs << 8) | bdd[o]);
+            }
+        }
+        return;
+    }
     uint8_t* Df = disp + (int64_t)frame * ostride;
 #pragma unroll
     for (int o = 0; o < G::SW2; ++o) {
@@ -431,6 +445,16 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         if (oy < H && x < W && h2s * G::SW2 + o < G::TW)
             Df[(int64_t)oy * out_pitch + x] = (uint8_t)(bdd[o] & 0xFF);   // (uchar)dm, Device.cu:63
     }
+}
+
+// Guided d-slice keys -> disparity: d where q < 50 (the Device.cu:37 seed, strict), else 0.
+// 50 * 2^14 is exact and the keys truncate q * 2^14, so (key >> 8) < 819200 iff q < 50.
+__global__ __launch_bounds__(256) void guided_keys_to_disp_kernel(const int* __restrict__ keys, int W, int H,
+                                                                  uint8_t* __restrict__ disp, int out_pitch) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int k = keys[(int64_t)y * W + x];
+    disp[(int64_t)y * out_pitch + x] = (k >> 8) < (int)(50.0f * kRightScale) ? (uint8_t)(k & 0xFF) : (uint8_t)0;
 }
 
 // Right view of the fused pass: for each right pixel u of a tile row band, the minimum key over the
@@ -477,23 +501,23 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
 
 template <int R>
 hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch,
-                     int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride, int* gpart,
-                     uint8_t* right, int rpitch, int64_t rstride, hipStream_t s) {
+                     int d_lo, int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride,
+                     int* gpart, uint8_t* right, int rpitch, int64_t rstride, int* keys, hipStream_t s) {
     using G = GeoF<R>;
     const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     if (!gpart) {
         hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L,
-                           Rimg, W, H, pitch, fstride, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
-                           tiles_x * tiles_y, nullptr, 0);
+                           Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
+                           tiles_x * tiles_y, nullptr, 0, keys);
         return hipGetLastError();
     }
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
     hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg,
-                       W, H, pitch, fstride, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
-                       K);
+                       W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
+                       K, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(guided_right_reduce_kernel, dim3((unsigned)((W + 63) / 64), (unsigned)tiles_y, (unsigned)batch),
@@ -542,7 +566,7 @@ hipError_t launch_guided_match_lr(const uint8_t* L, const uint8_t* R, int W, int
     if (D < 1 || D > kMaxDisp) return hipErrorInvalidValue;
     if (gpart && (!right || valid_mode != 0)) return hipErrorInvalidValue;
 #define SM_GUIDED_CASE(r) \
-    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, D, eps, valid_mode, disp, out_pitch, out_frame_stride, gpart, right, rpitch, rstride, s)
+    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, 0, D, eps, valid_mode, disp, out_pitch, out_frame_stride, gpart, right, rpitch, rstride, nullptr, s)
     switch (radius) {
         SM_GUIDED_CASE(0);
         SM_GUIDED_CASE(1);
@@ -555,6 +579,33 @@ hipError_t launch_guided_match_lr(const uint8_t* L, const uint8_t* R, int W, int
         default: return hipErrorInvalidValue;
     }
 #undef SM_GUIDED_CASE
+}
+
+hipError_t launch_guided_slice_keys(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                    int64_t frame_stride, int radius, int d_lo, int d_hi, float eps, int* keys,
+                                    hipStream_t s) {
+    if (d_lo < 0 || d_hi <= d_lo || d_hi > kMaxDisp || !keys) return hipErrorInvalidValue;
+#define SM_GUIDED_SLICE(r) \
+    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, d_lo, d_hi, eps, 2, nullptr, 0, 0, nullptr, nullptr, 0, 0, keys, s)
+    switch (radius) {
+        SM_GUIDED_SLICE(0);
+        SM_GUIDED_SLICE(1);
+        SM_GUIDED_SLICE(2);
+        SM_GUIDED_SLICE(3);
+        SM_GUIDED_SLICE(4);
+        SM_GUIDED_SLICE(5);
+        SM_GUIDED_SLICE(6);
+        SM_GUIDED_SLICE(7);
+        default: return hipErrorInvalidValue;
+    }
+#undef SM_GUIDED_SLICE
+}
+
+hipError_t launch_guided_keys_to_disp(const int* keys, int W, int H, uint8_t* disp, int out_pitch, hipStream_t s) {
+    if (W <= 0 || H <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(guided_keys_to_disp_kernel, dim3((unsigned)((W + 255) / 256), (unsigned)H), dim3(256), 0, s,
+                       keys, W, H, disp, out_pitch);
+    return hipGetLastError();
 }
 
 }  // namespace sm

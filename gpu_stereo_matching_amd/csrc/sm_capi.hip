@@ -612,6 +612,32 @@ SM_API int sm_keys_to_disp_device(sm_handle* h, const uint32_t* d_keys, int widt
     return SM_OK;
 }
 
+SM_API int sm_guided_slice_keys_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width,
+                                       int height, int pitch, int radius, int d_lo, int d_hi, int32_t* d_keys,
+                                       void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, d_hi > 0 ? d_hi : 1);
+    if (rc) return rc;
+    if (radius > sm::kMaxFastRadius)
+        return fail(SM_ERR_INVALID_ARG, "guided aggregation: radius %d > %d", radius, sm::kMaxFastRadius);
+    if (d_lo < 0 || d_hi <= d_lo || d_hi > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "bad slice [%d,%d)", d_lo, d_hi);
+    if (!d_left || !d_right || !d_keys) return fail(SM_ERR_INVALID_ARG, "null device pointer");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_guided_slice_keys(d_left, d_right, width, height, pitch, 1, (int64_t)pitch * height, radius,
+                                        d_lo, d_hi, h->guided_eps, d_keys, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_guided_keys_to_disp_device(sm_handle* h, const int32_t* d_keys, int width, int height,
+                                         uint8_t* d_disp, int out_pitch, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_keys || !d_disp || width <= 0 || height <= 0 || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad guided_keys_to_disp arguments");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_guided_keys_to_disp(d_keys, width, height, d_disp, out_pitch, (hipStream_t)stream));
+    return SM_OK;
+}
+
 SM_API int sm_bgr_to_gray_device(sm_handle* h, const uint8_t* d_bgr, int width, int height, int pitch, int channels,
                                  uint8_t* d_gray, int gray_pitch, void* stream) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");

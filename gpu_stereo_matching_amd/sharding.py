@@ -102,16 +102,26 @@ def gather_disparity(chunk_u8, out_flat, group=None):
     return out_flat
 
 
+GUIDED_EMPTY_KEY = 0x7FFFFFFF   # guided slice key of a pixel with no valid d (INT32_MAX)
+
+
 def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int, world: int,
-                 keys_t=None, out_t=None, stream=None, group=None, collective: str = "rs_ag"):
+                 keys_t=None, out_t=None, stream=None, group=None, collective: str = "rs_ag", agg: str = "box"):
     """One frame, d-sharded over the process group: slice keys -> MIN reduce -> disparity.
 
     collective "rs_ag" (default): reduce-scatter the keys, convert this rank's chunk, all-gather
     uint8; "allreduce": MIN all-reduce of the whole key map, then convert.  keys_t / out_t: the
-    flat buffers of dslice_buffers() (allocated when None).  Returns the [H, W] disparity."""
+    flat buffers of dslice_buffers() (allocated when None).  agg "guided": the keys are the guided
+    path's signed (q * 2^14) << 8 | d (the same MIN collectives; padding / empty slices hold
+    INT32_MAX, the threshold q < 50 is applied after the reduction).  Returns the [H, W] disparity."""
     import torch
     if collective not in ("rs_ag", "allreduce"):
         raise ValueError("collective must be 'rs_ag' or 'allreduce'")
+    if agg not in ("box", "guided"):
+        raise ValueError("agg must be 'box' or 'guided'")
+    if agg == "guided":
+        return _match_dslice_guided(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream,
+                                    group, collective)
     lo, hi = dslice_bounds(num_disp, rank, world)
     H, W = left_t.shape[-2:]
     P = H * W
@@ -134,6 +144,35 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
     chunk = reduce_scatter_keys(keys_t, world, group)
     n = chunk.numel()
     mine = matcher.keys_to_disp_device(chunk.view(1, n), radius)
+    gather_disparity(mine.view(n), out_t, group)
+    return out_t[:P].view(H, W)
+
+
+def _match_dslice_guided(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream, group,
+                         collective):
+    import torch
+    lo, hi = dslice_bounds(num_disp, rank, world)
+    H, W = left_t.shape[-2:]
+    P = H * W
+    if keys_t is None or out_t is None:
+        keys_t, out_t = dslice_buffers(H, W, world, left_t.device)
+    if keys_t.numel() != padded_pixels(H, W, world) or out_t.numel() != keys_t.numel():
+        raise ValueError("keys_t / out_t must be dslice_buffers(H, W, world)")
+    keys_img = keys_t[:P].view(H, W)
+    if hi > lo:
+        matcher.guided_slice_keys_device(left_t, right_t, radius, lo, hi, keys_t=keys_img, stream=stream)
+    else:
+        keys_img.fill_(GUIDED_EMPTY_KEY)
+    keys_t[P:].fill_(GUIDED_EMPTY_KEY)
+    if stream is not None:
+        torch.cuda.current_stream(left_t.device).wait_stream(stream)
+    if collective == "allreduce":
+        reduce_slice_keys(keys_t, group)
+        matcher.guided_keys_to_disp_device(keys_t.view(1, -1), out_t=out_t.view(1, -1))
+        return out_t[:P].view(H, W)
+    chunk = reduce_scatter_keys(keys_t, world, group)
+    n = chunk.numel()
+    mine = matcher.guided_keys_to_disp_device(chunk.view(1, n))
     gather_disparity(mine.view(n), out_t, group)
     return out_t[:P].view(H, W)
 

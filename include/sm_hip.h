@@ -116,6 +116,20 @@ SM_API int sm_slice_keys_device(sm_handle *h, const uint8_t *d_left, const uint8
 SM_API int sm_keys_to_disp_device(sm_handle *h, const uint32_t *d_keys, int width, int height,
                                   int radius, uint8_t *d_disp, int out_pitch, void *stream);
 
+/* Guided-aggregation d-slice keys (the same sharding over d for SM_AGG_GUIDED): per pixel the
+ * best d in [d_lo, d_hi) (valid d <= W - x, no threshold) of the guided-filtered cost q, as
+ * ((int32)(q * 2^14) << 8) | d; INT32_MAX where no d of the slice is valid.  Keys of disjoint
+ * slices combine with an elementwise SIGNED min (q may be negative).  The handle's guided eps
+ * applies.  The combined map equals the single-device guided map up to the 2^-14 quantisation of q
+ * (near-ties of the fp32 costs may resolve to the other d). */
+SM_API int sm_guided_slice_keys_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right,
+                                       int width, int height, int pitch, int radius, int d_lo, int d_hi,
+                                       int32_t *d_keys, void *stream);
+
+/* Guided key map -> disparity: d where q < 50 (the Device.cu:37 seed, strict), else 0. */
+SM_API int sm_guided_keys_to_disp_device(sm_handle *h, const int32_t *d_keys, int width, int height,
+                                         uint8_t *d_disp, int out_pitch, void *stream);
+
 /* Wait for all work queued on `stream` (NULL = the handle's own stream). */
 SM_API int sm_stream_sync(sm_handle *h, void *stream);
 
