@@ -177,20 +177,37 @@ def _match_dslice_guided(matcher, left_t, right_t, radius, num_disp, rank, world
     return out_t[:P].view(H, W)
 
 
-def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_ag", group=None):
+GUIDED_SEED_Q = 50 * 16384   # q < 50 in the guided keys' 2^-14 fixed point (Device.cu:37 seed)
+
+
+def guided_keys_to_disparity_host(keys):
+    """numpy twin of sm_guided_keys_to_disp_device: signed key map -> d where q < 50, else 0."""
+    import numpy as np
+    k = np.asarray(keys, np.int32)
+    return np.where((k >> 8) < GUIDED_SEED_Q, k & 0xFF, 0).astype(np.uint8)
+
+
+def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_ag", group=None, agg: str = "box"):
     """CPU (gloo) form of match_dslice's reduction for tests: this rank's [H, W] slice keys (int32
-    numpy) -> the [H, W] uint8 disparity of the global minimum, through the same collectives."""
+    numpy) -> the [H, W] uint8 disparity of the global minimum, through the same collectives.
+    agg "guided": signed guided keys, INT32_MAX padding, threshold q < 50."""
     import numpy as np
     import torch
     H, W = keys.shape
     P = H * W
-    flat = torch.full((padded_pixels(H, W, world),), seed_key(radius), dtype=torch.int32)
+    if agg == "guided":
+        fill = GUIDED_EMPTY_KEY
+        finish = lambda k: guided_keys_to_disparity_host(k)   # noqa: E731
+    else:
+        fill = seed_key(radius)
+        finish = lambda k: keys_to_disparity_host(k.view(np.uint32), radius)   # noqa: E731
+    flat = torch.full((padded_pixels(H, W, world),), fill, dtype=torch.int32)
     flat[:P] = torch.from_numpy(np.ascontiguousarray(keys, np.int32).reshape(P))
     if collective == "allreduce":
         reduce_slice_keys(flat, group)
-        return keys_to_disparity_host(flat.numpy()[:P].view(np.uint32), radius).reshape(H, W)
+        return finish(flat.numpy()[:P]).reshape(H, W)
     chunk = reduce_scatter_keys(flat, world, group)
-    mine = torch.from_numpy(keys_to_disparity_host(chunk.numpy().view(np.uint32), radius))
+    mine = torch.from_numpy(finish(chunk.numpy()))
     out = torch.empty(flat.numel(), dtype=torch.uint8)
     gather_disparity(mine, out, group)
     return out.numpy()[:P].reshape(H, W)

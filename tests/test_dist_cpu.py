@@ -61,6 +61,51 @@ def test_dslice_min_reduction_gloo(tmp_path, world, D, W):
         assert (np.load(tmp_path / f"frames{k}.npy") == 1).all()
 
 
+def _guided_slice_keys(q, lo, hi):
+    """Host restatement of sm_guided_slice_keys_device on the oracle's fp64 q volume [D][H][W]:
+    (int)(q * 2^14) << 8 | d over the valid d (d <= W - x) of [lo, hi), INT32_MAX if none."""
+    _, H, W = q.shape
+    xs = np.arange(W)[None, :]
+    best = np.full((H, W), sharding.GUIDED_EMPTY_KEY, np.int64)
+    for d in range(lo, hi):
+        k = (np.trunc(np.clip(q[d] * 16384.0, -2 ** 23, 2 ** 23 - 1)).astype(np.int64) << 8) | d
+        best = np.where(d <= W - xs, np.minimum(best, k), best)
+    return best.astype(np.int32)
+
+
+def _guided_worker(rank, world, port, W, H, r, D, result_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q = np.load(os.path.join(result_dir, "q.npy"))
+    lo, hi = sharding.dslice_bounds(D, rank, world)
+    keys = _guided_slice_keys(q, lo, hi)
+    for coll in ("allreduce", "rs_ag"):
+        disp = sharding.match_dslice_host_keys(keys, r, world, collective=coll, agg="guided")
+        np.save(os.path.join(result_dir, f"g{rank}_{coll}.npy"), disp)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,D,W", [(2, 32, 61), (3, 5, 40)])
+def test_guided_dslice_reduction_gloo(tmp_path, world, D, W):
+    """Guided d-slices: the signed key MIN (negative q included) through both collectives, INT32_MAX
+    padding and empty slices, then q < 50, equals the full-range keys' map and the fp64 oracle's
+    disparity wherever the oracle's best two costs are not within the 2^-14 key quantum."""
+    from oracle import oracle as O
+    H, r, eps = 23, 2, 1e-4 * 255 * 255
+    L, R = O.synth_pair(99, W, H, 16)
+    disp_o, q, best = O.guided_disp(L, R, r, D, eps, want_q=True)
+    np.save(tmp_path / "q.npy", q)
+    assert (q < 0).any()   # the guided cost can be negative: the MIN must be signed
+    port = _free_port()
+    mp.spawn(_guided_worker, args=(world, port, W, H, r, D, str(tmp_path)), nprocs=world, join=True)
+    want = sharding.guided_keys_to_disparity_host(_guided_slice_keys(q, 0, D))
+    assert (want == disp_o).mean() > 0.99
+    for k in range(world):
+        for coll in ("allreduce", "rs_ag"):
+            assert np.array_equal(np.load(tmp_path / f"g{k}_{coll}.npy"), want), (k, coll)
+
+
 def test_shard_helpers():
     assert sharding.dslice_bounds(128, 0, 8) == (0, 16)
     assert sharding.dslice_bounds(128, 7, 8) == (112, 128)
