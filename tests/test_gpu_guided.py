@@ -199,3 +199,29 @@ def test_guided_dslice_one_rccl_rank(oracle, torch):
                 assert (got.cpu().numpy() == full.cpu().numpy()).mean() > 0.998, coll
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H,D,r,cuts", [(300, 45, 256, 5, [0, 100, 256]), (61, 19, 100, 2, [0, 33, 34, 100]),
+                                          (97, 40, 64, 7, [0, 31, 32, 63, 64])])
+def test_guided_slice_keys_ragged(matcher, oracle, torch, W, H, D, r, cuts):
+    """Slices up to d_max = 256, one-disparity slices, band-chunk edges (32) and slices wholly past
+    the valid range of the right border columns, on ragged frames: same contract as above."""
+    L, R = oracle.synth_pair(W * 7 + H, W, H, min(D, 64))
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    parts = [matcher.guided_slice_keys_device(Lt, Rt, r, a, b) for a, b in zip(cuts[:-1], cuts[1:])]
+    k = parts[0].clone()
+    for p in parts[1:]:
+        k = torch.minimum(k, p)
+    got = matcher.guided_keys_to_disp_device(k)
+    torch.cuda.synchronize()
+    xs = np.arange(W)[None, :]
+    for (a, b), p in zip(zip(cuts[:-1], cuts[1:]), parts):
+        pk = p.cpu().numpy()
+        empty = pk == 0x7FFFFFFF
+        d = pk & 0xFF
+        assert ((d >= a) & (d < b) & (d <= W - xs))[~empty].all(), (a, b)
+        assert (empty == (a > W - xs)).all(), (a, b)
+    got = got.cpu().numpy()
+    disp_o, q, best = oracle.guided_disp(L, R, r, D, EPS, want_q=True)
+    ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, D, W)
+    assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
