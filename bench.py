@@ -14,7 +14,8 @@ shard frames with no data-path collective ("scaling": "weak").  The two single-f
 SURVEY §8e are measured in the same run for N > 1: "dslice" (cfg4: each rank owns a disparity
 slice of the SAME 1080p d_max=256 frame; packed-key MIN reduce-scatter + uint8 all-gather over
 RCCL, and the plain MIN all-reduce beside it) and "rowband" (each rank owns a band of rows plus an
-r-row halo, all-gather of the uint8 bands).
+r-row halo, all-gather of the uint8 bands).  "cfg5_guided_lr" (every N) is BASELINE configs[4] as
+written: 4K pairs, d_max=192, guided filter + LR check, frames batched over all ranks.
 
 Rank 0 prints ONE JSON line.  Timing: barrier + synchronize on both sides of exactly K steps,
 max over ranks.  The dominant kernel's duration is measured live with HIP events on the stream
@@ -51,6 +52,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip the per-config / LR / guided table")
     ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the 4K guided+LR frame-parallel block")
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (what rocprof summaries under profiles/ are taken from)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_box_r5_1080p.json"))
@@ -225,7 +227,7 @@ def cpu_baseline_all_cores(W, H, D, r, seed):
 def main():
     args = parse()
     if args.profile:
-        args.no_cpu_baseline = args.no_variants = args.no_latency = True
+        args.no_cpu_baseline = args.no_variants = args.no_latency = args.no_cfg5 = True
     import torch
     import torch.distributed as dist
 
@@ -361,6 +363,46 @@ def main():
                    "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_gather uint8 bands ({backend})",
                    "halo_rows": r, "scaling": "strong"}
 
+    # ---- cfg5 as BASELINE configs[4] writes it: 4K pairs, d_max=192, guided + LR, frames batched
+    #      over every rank (frame-parallel, no collective), whole-job maps/s with the max-over-ranks clock ----
+    cfg5 = None
+    if not args.no_cfg5:
+        W5, H5, D5, B5 = 3840, 2160, 192, 2
+        m5 = sm.BlockMatcher(dev_index, W5, H5, 256)
+        try:
+            p5 = [sm.synth_pair(4321 + rank * B5 + i, W5, H5, D5) for i in range(B5)]
+            L5 = torch.from_numpy(np.stack([p[0] for p in p5])).to(dev)
+            R5 = torch.from_numpy(np.stack([p[1] for p in p5])).to(dev)
+            o5 = torch.empty_like(L5)
+
+            def step5():
+                m5.match_device(L5, R5, r, D5, out_t=o5, agg="guided", lr_check=True, stream=stream)
+
+            for _ in range(2):
+                step5()
+            n5 = max(5, args.steps // 10)
+            if distributed:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(n5):
+                step5()
+            torch.cuda.synchronize(dev)
+            if distributed:
+                dist.barrier()
+            dt5 = time.perf_counter() - t1
+            if distributed:
+                t = torch.tensor([dt5], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt5 = float(t.item())
+            cfg5 = {"config": f"cfg5: {W5}x{H5} synthetic pairs (seeds 4321+frame), {2*r+1}x{2*r+1} guided-filter "
+                              f"aggregation + LR check, d_max={D5}, {B5} frames per launch per GPU, frame-parallel "
+                              f"x{world}", "value": round(B5 * world * n5 / dt5, 2), "unit": "disparity-maps/s",
+                    "ms_per_step": round(dt5 * 1000 / n5, 4), "steps": n5, "n_gpus": world, "scaling": "weak",
+                    "kernel": "guided_fused_kernel<5, true>", "dtype": "fp32 (u8 in/out)"}
+        finally:
+            m5.close()
+
     # ---- BASELINE configs, LR and guided variants on rank 0 ----
     variants = None
     if rank == 0 and not args.no_variants:
@@ -417,6 +459,8 @@ def main():
             res["dslice"] = dslice
         if rowband is not None:
             res["rowband"] = rowband
+        if cfg5 is not None:
+            res["cfg5_guided_lr"] = cfg5
         if variants:
             res["variants"] = variants
             # BASELINE configs[2] as written (11x11 + guided-filter aggregation, 1080p d_max=128),
