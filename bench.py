@@ -474,6 +474,14 @@ def main():
                                       "with_lr_check": {"value": glr.get("maps_per_s"),
                                                         "ms_per_frame": glr.get("ms_per_frame")},
                                       "kernel": "guided_fused_kernel<5>", "dtype": "fp32 (u8 in/out)"}
+                # the same algorithmic-bytes roofline as the headline (P*(2D+3) per map); the guided
+                # kernel reads only the pair and writes the map, and is VALU/LDS-bound
+                ga = bpm / (g["ms_per_frame"] * 1e-3) / 1e9
+                res["cfg3_guided"]["roofline"] = {
+                    "bound": "hbm", "achieved": round(ga, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ga / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_map": bpm,
+                    "note": "compute-bound in fact: ~60-70 % VALU and ~60 % LDS busy per PMC "
+                            "(profiles/pmc_guided_counters_r5_1080p.json)"}
         print(json.dumps(res), flush=True)
 
     m.close()
