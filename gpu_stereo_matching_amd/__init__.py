@@ -53,6 +53,21 @@ def _flags(agg: str, lr_check: bool, median: bool = False) -> int:
     return f | (SM_LR_CHECK if lr_check else 0) | (SM_MEDIAN if median else 0)
 
 
+def _check_device_pair(left_t, right_t, keys_t=None):
+    """[H, W] uint8 contiguous device frames of one shape (and an int32 [H, W] key map when given):
+    the C ABI takes raw pointers and cannot check what they point at."""
+    import torch
+    if left_t.dtype != torch.uint8 or right_t.dtype != torch.uint8:
+        raise ValueError("expected uint8 tensors")
+    if left_t.shape != right_t.shape or left_t.dim() != 2:
+        raise ValueError("left/right must be equal [H, W] tensors")
+    if not (left_t.is_cuda and right_t.is_cuda and left_t.is_contiguous() and right_t.is_contiguous()):
+        raise ValueError("expected contiguous device tensors")
+    if keys_t is not None and (keys_t.dtype != torch.int32 or tuple(keys_t.shape) != tuple(left_t.shape)
+                               or not keys_t.is_contiguous() or keys_t.device != left_t.device):
+        raise ValueError("keys_t must be a contiguous int32 [H, W] tensor on the frames' device")
+
+
 class BlockMatcher:
     """One device handle: pre-allocated buffers + a HIP stream (``sm_create``)."""
 
@@ -283,6 +298,7 @@ class BlockMatcher:
         H, W = left_t.shape[-2:]
         if keys_t is None:
             keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        _check_device_pair(left_t, right_t, keys_t)
         _capi.check(self._lib.sm_slice_keys_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, radius,
                                                    d_lo, d_hi, keys_t.data_ptr(), self._stream_ptr(stream)))
         return keys_t
@@ -304,6 +320,7 @@ class BlockMatcher:
         H, W = left_t.shape[-2:]
         if keys_t is None:
             keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        _check_device_pair(left_t, right_t, keys_t)
         _capi.check(self._lib.sm_guided_slice_keys_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W,
                                                           radius, d_lo, d_hi, keys_t.data_ptr(),
                                                           self._stream_ptr(stream)))

@@ -49,3 +49,18 @@ def test_api_rejects_bad_images():
     with pytest.raises(ValueError):
         sm._flags("median", False)
     assert sm._flags("guided", True) == sm.SM_AGG_GUIDED | sm.SM_LR_CHECK
+
+
+def test_device_pair_checks_reject_bad_inputs():
+    """The slice-key wrappers validate what the C ABI cannot (dtype, rank, shape, device, contiguity)."""
+    import torch
+    import gpu_stereo_matching_amd as sm
+    a = torch.zeros((4, 8), dtype=torch.uint8)
+    with pytest.raises(ValueError, match="uint8"):
+        sm._check_device_pair(a.float(), a)
+    with pytest.raises(ValueError, match="equal"):
+        sm._check_device_pair(a, torch.zeros((4, 9), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="equal"):
+        sm._check_device_pair(a[None], a[None])
+    with pytest.raises(ValueError, match="device"):
+        sm._check_device_pair(a, a)
