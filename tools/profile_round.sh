@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 timeout -k 10 900 python tools/pmc_traffic.py box_r5_1080p > gpurun_out/${TAG}_pmc.txt 2>&1 \
  && timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
  && cat gpurun_out/${TAG}_bench.json \
- && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o bench --output-format csv -- python3 bench.py --profile > gpurun_out/${TAG}_prof_bench.json 2>&1 \
+ && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o bench --output-format csv -- python3 bench.py --profile > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof_bench.err \
  && cat gpurun_out/${TAG}_prof_bench.json \
  && cat $(find gpurun_out/${TAG}_prof -name '*kernel_stats.csv' | head -1) | cut -c1-180 \
  && echo PROFILE_OK
