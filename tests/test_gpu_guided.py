@@ -225,3 +225,37 @@ def test_guided_slice_keys_ragged(matcher, oracle, torch, W, H, D, r, cuts):
     disp_o, q, best = oracle.guided_disp(L, R, r, D, EPS, want_q=True)
     ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, D, W)
     assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
+
+
+def test_guided_pitched_host_input(matcher, gray):
+    """Row pitch > width (a Mat ROI) on the guided path: the padding bytes (random, not zero) are never
+    read, so the map is bit-identical to the contiguous call; the output pitch is honoured."""
+    import gpu_stereo_matching_amd as sm
+    L, R = gray["Art/view1"], gray["Art/view5"]
+    H, W = L.shape
+    P = W + 29
+    rng = np.random.default_rng(3)
+    Lp = rng.integers(0, 256, (H, P), dtype=np.uint8)
+    Rp = rng.integers(0, 256, (H, P), dtype=np.uint8)
+    Lp[:, :W] = L
+    Rp[:, :W] = R
+    out = np.full((H, W + 3), 9, np.uint8)
+    rc = matcher._lib.sm_block_match_u8(matcher._h, Lp.ctypes.data, Rp.ctypes.data, W, H, P, 4, 64,
+                                        sm.SM_AGG_GUIDED, out.ctypes.data, W + 3)
+    assert rc == 0
+    assert np.array_equal(out[:, :W], matcher.match(L, R, 4, 64, agg="guided"))
+    assert (out[:, W:] == 9).all()
+
+
+@pytest.mark.parametrize("eps", [1.0, 5000.0])
+def test_guided_eps_parameter(oracle, gray, eps):
+    """SM_PARAM_GUIDED_EPS reaches the kernel: other eps values, tie-aware against the fp64 oracle."""
+    import gpu_stereo_matching_amd as sm
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    with sm.BlockMatcher(0, 640, 480, 256) as m:
+        m.set_guided_eps(eps)
+        got = m.match(L, R, 3, 48, agg="guided")
+    disp_o, q, best = oracle.guided_disp(L, R, 3, 48, eps, want_q=True)
+    ok, exact = tie_aware_check(got, q, {"disp": disp_o, "best": best}, 48, L.shape[1])
+    assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
+    assert exact.mean() > 0.99
