@@ -411,3 +411,49 @@ def test_staged_median_batch(matcher, oracle, torch):
     torch.cuda.synchronize()
     for b in range(3):
         assert np.array_equal(out[b].cpu().numpy(), oracle.median(oracle.box_disp(pairs[b][0], pairs[b][1], 3, 32), 3))
+
+
+def _fuzz_pair(rng, W, H):
+    """Random texture with flat patches, saturated 0 / 255 runs and a shifted right view: exercises
+    ties (flat regions: equal SADs over many d), the u16 packed sums at their extremes, and borders."""
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    kind = rng.integers(0, 4)
+    if kind == 1:
+        L[:, : W // 2] = rng.integers(0, 256)                      # flat half: many exact ties
+    elif kind == 2:
+        L = np.where(rng.random((H, W)) < 0.5, 0, 255).astype(np.uint8)   # saturated values only
+    elif kind == 3:
+        L = (L // 64 * 64).astype(np.uint8)                         # 4 levels: frequent ties
+    s = int(rng.integers(0, 20))
+    R = np.roll(L, -s, axis=1)
+    noise = rng.integers(-3, 4, (H, W))
+    R = np.clip(R.astype(np.int32) + noise * (rng.random((H, W)) < 0.3), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(L), np.ascontiguousarray(R)
+
+
+@pytest.mark.parametrize("seed", list(range(40)))
+def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
+    """Seeded random shapes / radii / disparity counts / textures: box (host and batched device),
+    box + LR, and the MIN over random d-slices, all bit-exact against the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    W, H = int(rng.integers(1, 700)), int(rng.integers(1, 120))
+    r, D = int(rng.integers(0, 10)), int(rng.integers(1, 257))
+    L, R = _fuzz_pair(rng, W, H)
+    disp, keys = oracle.box_disp(L, R, r, D, want_keys=True)
+    assert np.array_equal(matcher.match(L, R, r, D), disp), (W, H, r, D)
+    L2, R2 = _fuzz_pair(rng, W, H)
+    Lt = torch.from_numpy(np.stack([L, L2])).cuda()
+    Rt = torch.from_numpy(np.stack([R, R2])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D).cpu().numpy()
+    assert np.array_equal(out[0], disp) and np.array_equal(out[1], oracle.box_disp(L2, R2, r, D)), (W, H, r, D)
+    _, rd, chk, mask = oracle.box_lr(L, R, r, D)
+    c, rr, mm = matcher.match_lr(L, R, r, D)
+    assert np.array_equal(rr, rd) and np.array_equal(c, chk) and np.array_equal(mm, mask), (W, H, r, D)
+    if r <= 7:
+        cuts = sorted({0, D, *[int(v) for v in rng.integers(1, D + 1, size=3)]})
+        k = None
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            p = matcher.slice_keys_device(Lt[0], Rt[0], r, a, b)
+            k = p if k is None else torch.minimum(k, p)
+        torch.cuda.synchronize()
+        assert np.array_equal(k.cpu().numpy().view(np.uint32), keys), (W, H, r, D, cuts)
