@@ -6,6 +6,7 @@ fast oracle formulation (ora_box_disp, O(P*D)).
 """
 import numpy as np
 import pytest
+from fuzz_util import fuzz_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -413,24 +414,6 @@ def test_staged_median_batch(matcher, oracle, torch):
         assert np.array_equal(out[b].cpu().numpy(), oracle.median(oracle.box_disp(pairs[b][0], pairs[b][1], 3, 32), 3))
 
 
-def _fuzz_pair(rng, W, H):
-    """Random texture with flat patches, saturated 0 / 255 runs and a shifted right view: exercises
-    ties (flat regions: equal SADs over many d), the u16 packed sums at their extremes, and borders."""
-    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
-    kind = rng.integers(0, 4)
-    if kind == 1:
-        L[:, : W // 2] = rng.integers(0, 256)                      # flat half: many exact ties
-    elif kind == 2:
-        L = np.where(rng.random((H, W)) < 0.5, 0, 255).astype(np.uint8)   # saturated values only
-    elif kind == 3:
-        L = (L // 64 * 64).astype(np.uint8)                         # 4 levels: frequent ties
-    s = int(rng.integers(0, 20))
-    R = np.roll(L, -s, axis=1)
-    noise = rng.integers(-3, 4, (H, W))
-    R = np.clip(R.astype(np.int32) + noise * (rng.random((H, W)) < 0.3), 0, 255).astype(np.uint8)
-    return np.ascontiguousarray(L), np.ascontiguousarray(R)
-
-
 @pytest.mark.parametrize("seed", list(range(40)))
 def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
     """Seeded random shapes / radii / disparity counts / textures: box (host and batched device),
@@ -438,10 +421,10 @@ def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
     rng = np.random.default_rng(1000 + seed)
     W, H = int(rng.integers(1, 700)), int(rng.integers(1, 120))
     r, D = int(rng.integers(0, 10)), int(rng.integers(1, 257))
-    L, R = _fuzz_pair(rng, W, H)
+    L, R = fuzz_pair(rng, W, H)
     disp, keys = oracle.box_disp(L, R, r, D, want_keys=True)
     assert np.array_equal(matcher.match(L, R, r, D), disp), (W, H, r, D)
-    L2, R2 = _fuzz_pair(rng, W, H)
+    L2, R2 = fuzz_pair(rng, W, H)
     Lt = torch.from_numpy(np.stack([L, L2])).cuda()
     Rt = torch.from_numpy(np.stack([R, R2])).cuda()
     out = matcher.match_device(Lt, Rt, r, D).cpu().numpy()
