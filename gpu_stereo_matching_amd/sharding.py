@@ -48,7 +48,8 @@ def _host_staged(group) -> bool:
 
 
 def reduce_slice_keys(keys, group=None):
-    """In-place MIN all-reduce of an int32 key map (keys < 2^31 by construction)."""
+    """In-place signed MIN all-reduce of an int32 key map (box keys are < 2^31 by construction, guided
+    keys carry a signed cost)."""
     import torch.distributed as dist
     if keys.is_cuda and _host_staged(group):
         h = keys.cpu()
@@ -117,11 +118,18 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
     import torch
     if collective not in ("rs_ag", "allreduce"):
         raise ValueError("collective must be 'rs_ag' or 'allreduce'")
-    if agg not in ("box", "guided"):
+    if agg == "box":
+        fill = seed_key(radius)
+        slice_keys = lambda lo, hi, k: matcher.slice_keys_device(left_t, right_t, radius, lo, hi,  # noqa: E731
+                                                                 keys_t=k, stream=stream)
+        to_disp = lambda k, o=None: matcher.keys_to_disp_device(k, radius, out_t=o)  # noqa: E731
+    elif agg == "guided":
+        fill = GUIDED_EMPTY_KEY
+        slice_keys = lambda lo, hi, k: matcher.guided_slice_keys_device(left_t, right_t, radius, lo, hi,  # noqa: E731
+                                                                        keys_t=k, stream=stream)
+        to_disp = lambda k, o=None: matcher.guided_keys_to_disp_device(k, out_t=o)  # noqa: E731
+    else:
         raise ValueError("agg must be 'box' or 'guided'")
-    if agg == "guided":
-        return _match_dslice_guided(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream,
-                                    group, collective)
     lo, hi = dslice_bounds(num_disp, rank, world)
     H, W = left_t.shape[-2:]
     P = H * W
@@ -131,48 +139,19 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
         raise ValueError("keys_t / out_t must be dslice_buffers(H, W, world)")
     keys_img = keys_t[:P].view(H, W)
     if hi > lo:
-        matcher.slice_keys_device(left_t, right_t, radius, lo, hi, keys_t=keys_img, stream=stream)
+        slice_keys(lo, hi, keys_img)
     else:
-        keys_img.fill_(seed_key(radius))
-    keys_t[P:].fill_(seed_key(radius))
+        keys_img.fill_(fill)
+    keys_t[P:].fill_(fill)
     if stream is not None:
         torch.cuda.current_stream(left_t.device).wait_stream(stream)
     if collective == "allreduce":
         reduce_slice_keys(keys_t, group)
-        matcher.keys_to_disp_device(keys_t.view(1, -1), radius, out_t=out_t.view(1, -1))
+        to_disp(keys_t.view(1, -1), out_t.view(1, -1))
         return out_t[:P].view(H, W)
     chunk = reduce_scatter_keys(keys_t, world, group)
     n = chunk.numel()
-    mine = matcher.keys_to_disp_device(chunk.view(1, n), radius)
-    gather_disparity(mine.view(n), out_t, group)
-    return out_t[:P].view(H, W)
-
-
-def _match_dslice_guided(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream, group,
-                         collective):
-    import torch
-    lo, hi = dslice_bounds(num_disp, rank, world)
-    H, W = left_t.shape[-2:]
-    P = H * W
-    if keys_t is None or out_t is None:
-        keys_t, out_t = dslice_buffers(H, W, world, left_t.device)
-    if keys_t.numel() != padded_pixels(H, W, world) or out_t.numel() != keys_t.numel():
-        raise ValueError("keys_t / out_t must be dslice_buffers(H, W, world)")
-    keys_img = keys_t[:P].view(H, W)
-    if hi > lo:
-        matcher.guided_slice_keys_device(left_t, right_t, radius, lo, hi, keys_t=keys_img, stream=stream)
-    else:
-        keys_img.fill_(GUIDED_EMPTY_KEY)
-    keys_t[P:].fill_(GUIDED_EMPTY_KEY)
-    if stream is not None:
-        torch.cuda.current_stream(left_t.device).wait_stream(stream)
-    if collective == "allreduce":
-        reduce_slice_keys(keys_t, group)
-        matcher.guided_keys_to_disp_device(keys_t.view(1, -1), out_t=out_t.view(1, -1))
-        return out_t[:P].view(H, W)
-    chunk = reduce_scatter_keys(keys_t, world, group)
-    n = chunk.numel()
-    mine = matcher.guided_keys_to_disp_device(chunk.view(1, n))
+    mine = to_disp(chunk.view(1, n))
     gather_disparity(mine.view(n), out_t, group)
     return out_t[:P].view(H, W)
 
