@@ -85,8 +85,10 @@ def cpu_baseline(W, H, D, r, seed):
 # synthetic pairs of the same size because /root/reference is not on the GPU box.
 VARIANTS = (
     # name, W, H, D, r, agg, lr, median, batch
-    ("cfg1 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, False, 16),
-    ("cfg2 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, False, 16),
+    # cfg1 / cfg2 on the reference's own bundled Middlebury pairs (Art, Books, Dolls; gray fixtures
+    # in tests/golden, 463x370 — BASELINE's "450x375"), cycled to 16 frames per launch
+    ("cfg1 Middlebury Art/Books/Dolls 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, False, 16),
+    ("cfg2 Middlebury Art/Books/Dolls 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, False, 16),
     # 1080p variants run 32 frames per launch like the headline, 4K 8 (the same ~8 rounds of
     # workgroups per launch): 4-frame launches lose 12-14 % to each launch's ramp-down
     ("cfg3 1080p 11x11 box+lr d128", 1920, 1080, 128, 5, "box", True, False, 32),
@@ -109,7 +111,12 @@ def run_variants(sm, torch, dev, stream, seed):
             try:
                 if (W, H, D, B) not in frames:
                     frames.clear()
-                    pairs = [sm.synth_pair(seed + i, W, H, D) for i in range(B)]
+                    if name.startswith(("cfg1 Middlebury", "cfg2 Middlebury")):
+                        g = np.load(os.path.join(ROOT, "tests", "golden", "middlebury_gray.npz"))
+                        scenes = ("Art", "Books", "Dolls")
+                        pairs = [(g[f"{scenes[i % 3]}/view1"], g[f"{scenes[i % 3]}/view5"]) for i in range(B)]
+                    else:
+                        pairs = [sm.synth_pair(seed + i, W, H, D) for i in range(B)]
                     frames[(W, H, D, B)] = (torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev),
                                             torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev))
                 Lt, Rt = frames[(W, H, D, B)]
