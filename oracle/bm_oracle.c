@@ -17,6 +17,9 @@
  *          cost volumes are d-major planes [D][H][W] (as Device.cu:193).
  */
 #include <stdint.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
@@ -347,6 +350,75 @@ ORA_API void ora_right_wta(const int32_t *cost, int W, int H, int D, uint8_t *ri
     }
 }
 
+/* Box left + right WTA in O(P) memory per thread (full-size LR checks, cfg5 at
+   3840x2160 D=192, without the D x P volume).  Left: ora_box_disp's rule.
+   Right: STMatching's C_R(y,u,d) = C_L(y,u+d,d) for u+d < W, else C_R(y,u,d-1)
+   (StereoHelper.cpp:156-180); the repeated value never wins a strict < again,
+   so the right WTA is the first argmin over d with u+d < W (:131-154).
+   OpenMP over contiguous d chunks; chunks merge in d order with strict <, so
+   ties keep the smaller d exactly as the sequential scan does. */
+ORA_API int ora_box_lr_probe(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                             uint8_t *left_out, uint8_t *right_out)
+{
+    const int64_t P = (int64_t)W * H;
+    const int win = 2 * radius + 1;
+    const int32_t T = 50 * win * win;
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    if (nt > D) nt = D;
+    if (nt < 1) nt = 1;
+    int32_t *bl = (int32_t *)malloc(sizeof(int32_t) * P * nt), *dl = (int32_t *)malloc(sizeof(int32_t) * P * nt);
+    int32_t *br = (int32_t *)malloc(sizeof(int32_t) * P * nt), *dr = (int32_t *)malloc(sizeof(int32_t) * P * nt);
+    int fail = !bl || !dl || !br || !dr;
+    if (!fail) {
+#pragma omp parallel num_threads(nt)
+        {
+            int t = 0;
+#ifdef _OPENMP
+            t = omp_get_thread_num();
+#endif
+            int d0 = (int)((int64_t)D * t / nt), d1 = (int)((int64_t)D * (t + 1) / nt);
+            int32_t *colsum = (int32_t *)malloc(sizeof(int32_t) * W);
+            int32_t *plane = (int32_t *)malloc(sizeof(int32_t) * P);
+            int32_t *b_l = bl + P * t, *d_l = dl + P * t, *b_r = br + P * t, *d_r = dr + P * t;
+            if (!colsum || !plane) {
+#pragma omp atomic write
+                fail = 1;
+            } else {
+                for (int64_t p = 0; p < P; ++p) { b_l[p] = T; d_l[p] = -256; b_r[p] = INT32_MAX; d_r[p] = 0; }
+                for (int d = d0; d < d1; ++d) {
+                    box_plane(L, R, W, H, radius, d, colsum, plane);
+                    for (int y = 0; y < H; ++y) {
+                        const int64_t row = (int64_t)y * W;
+                        for (int x = 0; x < W; ++x) {
+                            int32_t c = plane[row + x];
+                            if (x + d <= W && c < b_l[row + x]) { b_l[row + x] = c; d_l[row + x] = d; }
+                            int u = x - d;                  /* C_R(y, u, d) = C_L(y, x, d), u + d < W */
+                            if (u >= 0 && c < b_r[row + u]) { b_r[row + u] = c; d_r[row + u] = d; }
+                        }
+                    }
+                }
+            }
+            free(colsum); free(plane);
+        }
+    }
+    if (!fail) {
+        for (int64_t p = 0; p < P; ++p) {
+            int32_t bestl = bl[p], bdl = dl[p], bestr = br[p], bdr = dr[p];
+            for (int t = 1; t < nt; ++t) {
+                if (bl[P * t + p] < bestl) { bestl = bl[P * t + p]; bdl = dl[P * t + p]; }
+                if (br[P * t + p] < bestr) { bestr = br[P * t + p]; bdr = dr[P * t + p]; }
+            }
+            left_out[p] = (uint8_t)bdl;
+            right_out[p] = (uint8_t)bdr;
+        }
+    }
+    free(bl); free(dl); free(br); free(dr);
+    return fail ? -1 : 0;
+}
+
 ORA_API void ora_lr_check(const uint8_t *left_disp, const uint8_t *right_disp, int W, int H,
                           uint8_t *checked, uint8_t *valid_mask)
 {
@@ -381,7 +453,8 @@ ORA_API void ora_lr_check(const uint8_t *left_disp, const uint8_t *right_disp, i
 /* ------------------------------------------------------------------------- */
 static void box_mean_d(const double *src, int W, int H, int r, double *tmp, double *dst)
 {
-    /* vertical sums */
+    /* vertical sums (OpenMP over columns / rows: same per-pixel order of operations) */
+#pragma omp parallel for schedule(static)
     for (int x = 0; x < W; ++x) {
         double run = 0.0;
         for (int y = 0; y < r && y < H; ++y) run += src[(int64_t)y * W + x];
@@ -391,6 +464,7 @@ static void box_mean_d(const double *src, int W, int H, int r, double *tmp, doub
             tmp[(int64_t)y * W + x] = run;
         }
     }
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y) {
         int ny = (y + r < H ? y + r : H - 1) - (y - r > 0 ? y - r : 0) + 1;
         double run = 0.0;
@@ -409,6 +483,7 @@ static void box_mean_d(const double *src, int W, int H, int r, double *tmp, doub
    drift so the restatement is exact up to the final division. */
 static void box_mean_i(const int64_t *src, int W, int H, int r, int64_t *tmp, double *dst)
 {
+#pragma omp parallel for schedule(static)
     for (int x = 0; x < W; ++x) {
         int64_t run = 0;
         for (int y = 0; y < r && y < H; ++y) run += src[(int64_t)y * W + x];
@@ -418,6 +493,7 @@ static void box_mean_i(const int64_t *src, int W, int H, int r, int64_t *tmp, do
             tmp[(int64_t)y * W + x] = run;
         }
     }
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y) {
         int ny = (y + r < H ? y + r : H - 1) - (y - r > 0 ? y - r : 0) + 1;
         int64_t run = 0;
@@ -551,6 +627,7 @@ ORA_API int ora_guided_probe(const uint8_t *L, const uint8_t *R, int W, int H, i
         if (bestR) bestR[p] = 1e300;
     }
     for (int d = 0; d < D; ++d) {
+#pragma omp parallel for schedule(static)
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
                 int64_t p = (int64_t)y * W + x;
@@ -559,8 +636,10 @@ ORA_API int ora_guided_probe(const uint8_t *L, const uint8_t *R, int W, int H, i
                 isrc[p] = v;
             }
         box_mean_i(isrc, W, H, radius, itmp, mp);
+#pragma omp parallel for schedule(static)
         for (int64_t p = 0; p < P; ++p) isrc[p] *= L[p];
         box_mean_i(isrc, W, H, radius, itmp, mIp);
+#pragma omp parallel for schedule(static)
         for (int64_t p = 0; p < P; ++p) {
             double var = mII[p] - mI[p] * mI[p];
             double cov = mIp[p] - mI[p] * mp[p];
@@ -569,6 +648,8 @@ ORA_API int ora_guided_probe(const uint8_t *L, const uint8_t *R, int W, int H, i
         }
         box_mean_d(a, W, H, radius, dtmp, ma);
         box_mean_d(b, W, H, radius, dtmp, mb);
+        /* rows are independent: the right pixel u = x - d stays in row y */
+#pragma omp parallel for schedule(static)
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
                 int64_t p = (int64_t)y * W + x;

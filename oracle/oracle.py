@@ -64,6 +64,8 @@ def lib():
         L.ora_guided_probe.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_double, _u8p, _u8p, _u8p, _f64p, _f64p, _f64p, _f64p]
         L.ora_guided_probe.restype = ctypes.c_int
+        L.ora_box_lr_probe.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
+        L.ora_box_lr_probe.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -162,6 +164,18 @@ def box_lr(left, right, radius: int, D: int):
     """Full box + LR pipeline: (left disp, right disp, checked disp, valid mask)."""
     disp, cost = box_disp(left, right, radius, D, want_cost=True)
     rdisp = right_wta(cost)
+    checked, mask = lr_check(disp, rdisp)
+    return disp, rdisp, checked, mask
+
+
+def box_lr_probe(left, right, radius: int, D: int):
+    """box_lr in O(P) memory per thread (full-size LR checks): (left disp, right disp, checked, mask)."""
+    left, right = _img(left), _img(right)
+    H, W = left.shape
+    disp = np.empty((H, W), np.uint8)
+    rdisp = np.empty((H, W), np.uint8)
+    if lib().ora_box_lr_probe(_p(left, _u8p), _p(right, _u8p), W, H, radius, D, _p(disp, _u8p), _p(rdisp, _u8p)) != 0:
+        raise MemoryError("ora_box_lr_probe")
     checked, mask = lr_check(disp, rdisp)
     return disp, rdisp, checked, mask
 

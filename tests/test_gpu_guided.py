@@ -129,6 +129,39 @@ def test_guided_lr_full_cfg3(matcher, oracle):
     assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
 
 
+def test_guided_lr_full_cfg5():
+    """cfg5 exactly as BASELINE names it (configs[4]): 3840x2160, d_max = 192, guided filter + LR
+    check, r = 5, on the bench's synthetic pair (seed 4321), host call and 2-frame batched device
+    call.  Same rule as cfg3 above: both maps tie-aware within TOL against the fp64 oracle probed
+    at the GPU's maps, the checked map and mask bit-exact with StereoDisparity.cpp:136-147."""
+    import torch
+    import gpu_stereo_matching_amd as sm
+    from oracle import oracle
+    from guided_check import TOL
+    W, H, D, r = 3840, 2160, 192, 5
+    L, R = oracle.synth_pair(4321, W, H, D)
+    with sm.BlockMatcher(0, W, H, 256) as m:
+        m.set_guided_eps(EPS)
+        left = m.match(L, R, r, D, agg="guided")
+        chk, rd, mask = m.match_lr(L, R, r, D, agg="guided")
+        Lt = torch.from_numpy(np.stack([L, L])).cuda()
+        Rt = torch.from_numpy(np.stack([R, R])).cuda()
+        dev = m.match_device(Lt, Rt, r, D, agg="guided", lr_check=True)
+        torch.cuda.synchronize()
+        dev = dev.cpu().numpy()
+    assert np.array_equal(dev[0], chk) and np.array_equal(dev[1], chk)
+    disp_o, best, qL, bestR, qR = oracle.guided_probe(L, R, r, D, EPS, left, rd)
+    xs = np.arange(W)[None, :]
+    valid = left.astype(np.int64) <= (W - xs)
+    ok_l = (left == disp_o) | (valid & (qL <= best + TOL) & (qL < 50.0 + TOL)) | ((left == 0) & (best >= 50.0 - TOL))
+    assert ok_l.all(), f"left: {int((~ok_l).sum())} pixels outside the tie-aware tolerance"
+    assert (left == disp_o).mean() > 0.98
+    ok_r = qR <= bestR + TOL
+    assert ok_r.all(), f"right: {int((~ok_r).sum())} pixels outside the tie-aware tolerance"
+    chk_o, mask_o = oracle.lr_check(left, rd)
+    assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+
+
 def test_guided_lr_batched_device_and_median(matcher, oracle):
     """Batched device calls of the fused guided right view (per-frame right-key partials) give each
     frame's single-call result; with SM_MEDIAN both maps are filtered before the check."""

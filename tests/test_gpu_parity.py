@@ -149,6 +149,24 @@ def test_1080p_d256_and_4k_d192(matcher, oracle, torch):
         assert np.array_equal(out.cpu().numpy(), want), (W, H, D)
 
 
+def test_cfg5_box_lr_full_size(matcher, oracle, torch):
+    """BASELINE configs[4]'s frame size as written (3840x2160, d_max = 192, r = 5) through box + LR,
+    host call and batched device call: left map, right map (STMatching's C_R rule,
+    StereoHelper.cpp:131-180), checked map and mask bit-exact with the O(P) oracle."""
+    W, H, D, r = 3840, 2160, 192, 5
+    L, R = oracle.synth_pair(4321, W, H, D)
+    disp_o, rd_o, chk_o, mask_o = oracle.box_lr_probe(L, R, r, D)
+    assert np.array_equal(matcher.match(L, R, r, D), disp_o)
+    chk, rd, mask = matcher.match_lr(L, R, r, D)
+    assert np.array_equal(rd, rd_o), f"right: {int((rd != rd_o).sum())} pixels differ"
+    assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+    Lt = torch.from_numpy(np.stack([L, R])).cuda()
+    Rt = torch.from_numpy(np.stack([R, L])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D, lr_check=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[0].cpu().numpy(), chk_o)
+
+
 def test_lr_golden(matcher, gray, bm_expected):
     for k in [k for k in bm_expected.files if k.startswith("lr/") and k.endswith("/checked")]:
         _, p, r, D, _ = k.split("/")

@@ -60,6 +60,16 @@ def test_two_formulations_agree_random(oracle, shape, r, D):
     assert np.array_equal(oracle.get_disp(L, R, r, D), oracle.box_disp(L, R, r, D))
 
 
+@pytest.mark.parametrize("W,H,D,r", [(97, 40, 64, 3), (333, 77, 100, 5), (64, 20, 200, 0), (21, 13, 30, 2),
+                                     (1, 5, 8, 1), (300, 3, 256, 7)])
+def test_box_lr_probe_equals_volume_form(oracle, W, H, D, r):
+    """The O(P)-memory, d-chunk-parallel LR oracle (full-size cfg5 checks) equals the volume form
+    (ora_box_cost -> ora_right_wta -> ora_lr_check) bit for bit: chunk merges keep the smaller d."""
+    L, R = oracle.synth_pair(W * 31 + H, W, H, min(D, 64))
+    for a, b in zip(oracle.box_lr(L, R, r, D), oracle.box_lr_probe(L, R, r, D)):
+        assert np.array_equal(a, b)
+
+
 def test_key_slices_combine_by_min(oracle, gray):
     """Multi-GPU contract: min over d-slices of the packed keys == full-range key,
     and the finalised disparity equals the single-device map."""
