@@ -53,6 +53,13 @@ def _flags(agg: str, lr_check: bool, median: bool = False) -> int:
     return f | (SM_LR_CHECK if lr_check else 0) | (SM_MEDIAN if median else 0)
 
 
+def _check_out(out_t, shape, dtype, device, name: str = "out_t"):
+    """A caller-supplied output tensor: the C ABI writes prod(shape) elements through its raw pointer."""
+    if out_t.dtype != dtype or tuple(out_t.shape) != tuple(shape) or not out_t.is_contiguous() \
+            or out_t.device != device:
+        raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)} on {device}")
+
+
 def _check_device_pair(left_t, right_t, keys_t=None):
     """[H, W] uint8 contiguous device frames of one shape (and an int32 [H, W] key map when given):
     the C ABI takes raw pointers and cannot check what they point at."""
@@ -283,10 +290,13 @@ class BlockMatcher:
             raise ValueError("left/right must be equal [H,W] or [B,H,W]")
         if not (left_t.is_cuda and right_t.is_cuda and left_t.is_contiguous() and right_t.is_contiguous()):
             raise ValueError("expected contiguous device tensors")
+        if left_t.device != right_t.device or left_t.device.index != self.device:
+            raise ValueError(f"frames must be on cuda:{self.device}, the handle's device")
         B = 1 if left_t.dim() == 2 else left_t.shape[0]
         H, W = left_t.shape[-2:]
         if out_t is None:
             out_t = torch.empty_like(left_t)
+        _check_out(out_t, left_t.shape, torch.uint8, left_t.device)
         _capi.check(self._lib.sm_match_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, B, H * W,
                                               radius, num_disp, _flags(agg, lr_check, median), out_t.data_ptr(), W, H * W,
                                               self._stream_ptr(stream)))
@@ -306,8 +316,11 @@ class BlockMatcher:
     def keys_to_disp_device(self, keys_t, radius: int, out_t=None, stream=None):
         import torch
         H, W = keys_t.shape[-2:]
+        if keys_t.dtype != torch.int32 or not keys_t.is_cuda or not keys_t.is_contiguous():
+            raise ValueError("keys_t must be a contiguous int32 device tensor")
         if out_t is None:
             out_t = torch.empty((H, W), dtype=torch.uint8, device=keys_t.device)
+        _check_out(out_t.view(-1) if out_t.is_contiguous() else out_t, (H * W,), torch.uint8, keys_t.device)
         _capi.check(self._lib.sm_keys_to_disp_device(self._h, keys_t.data_ptr(), W, H, radius, out_t.data_ptr(), W,
                                                      self._stream_ptr(stream)))
         return out_t
@@ -330,8 +343,11 @@ class BlockMatcher:
         """Combined guided keys -> uint8 disparity (d where q < 50, else 0)."""
         import torch
         H, W = keys_t.shape[-2:]
+        if keys_t.dtype != torch.int32 or not keys_t.is_cuda or not keys_t.is_contiguous():
+            raise ValueError("keys_t must be a contiguous int32 device tensor")
         if out_t is None:
             out_t = torch.empty((H, W), dtype=torch.uint8, device=keys_t.device)
+        _check_out(out_t.view(-1) if out_t.is_contiguous() else out_t, (H * W,), torch.uint8, keys_t.device)
         _capi.check(self._lib.sm_guided_keys_to_disp_device(self._h, keys_t.data_ptr(), W, H, out_t.data_ptr(), W,
                                                             self._stream_ptr(stream)))
         return out_t

@@ -50,6 +50,12 @@ struct sm_handle {
     uint8_t* d_bgr = nullptr;
     size_t bgr_bytes = 0;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
+    // The workspaces above are shared by every call on the handle while calls run on the stream
+    // they are given: the end of each pass is recorded here, and a pass on another stream waits
+    // for it first, so two streams never write the same workspace at once.
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_pending = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float stage_ms[3] = {0.f, 0.f, 0.f};
 };
@@ -178,9 +184,9 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
 //               the left costs, bm_guided.hip); box r > 7 matches the mirrored pair (valid d <= x,
 //               no threshold) and keeps it mirrored;
 //   LR check  : StereoDisparity.cpp:136-147 on the (median-filtered, :119-126) maps.
-int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
-               int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
-               uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
+int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                    int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
+                    uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
     const bool lr = (flags & SM_LR_CHECK) != 0 || right_out || mask_out;
     const bool med = (flags & SM_MEDIAN) != 0;
@@ -285,6 +291,20 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     SM_HIP(sm::launch_lr_check(disp, opitch, ostride, rcheck, W, P, mirrored ? 1 : 0, W, H, batch, disp, opitch,
                                ostride, right_out, mask_out, apitch, astride, s));
     return SM_OK;
+}
+
+// run_device_body on stream s, ordered after the handle's previous pass when that ran on another
+// stream (the workspaces d_lr / d_rpart / d_vol are per handle).
+int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+               int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
+               uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
+    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    const int rc = run_device_body(h, L, R, W, H, pitch, batch, fstride, radius, D, flags, disp, opitch, ostride,
+                                   right_out, mask_out, apitch, astride, s);
+    SM_HIP(hipEventRecord(h->scratch_ev, s));
+    h->scratch_stream = s;
+    h->scratch_pending = true;
+    return rc;
 }
 
 // Host-pointer pass over one frame (or one row band of a frame: sm_group_*).  Only result rows
@@ -497,6 +517,7 @@ SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm
     if (e == hipSuccess) e = hipMalloc(&h->d_right, P);
     if (e == hipSuccess) e = hipMalloc(&h->d_disp, P);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         sm_destroy(h);
         return fail(e == hipErrorOutOfMemory ? SM_ERR_OUT_OF_MEMORY : SM_ERR_DEVICE, "sm_create: %s",
@@ -510,6 +531,7 @@ SM_API int sm_destroy(sm_handle* h) {
     if (!h) return SM_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->scratch_ev && h->scratch_pending) (void)hipEventSynchronize(h->scratch_ev);   // device calls on other streams
     (void)hipFree(h->d_left);
     (void)hipFree(h->d_right);
     (void)hipFree(h->d_disp);
@@ -521,6 +543,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_bgr);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SM_OK;
@@ -893,7 +916,14 @@ SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const ui
 SM_API int sm_stream_sync(sm_handle* h, void* stream) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
     SM_HIP(hipSetDevice(h->device));
-    SM_HIP(hipStreamSynchronize(stream ? (hipStream_t)stream : h->stream));
+    if (stream) {
+        SM_HIP(hipStreamSynchronize((hipStream_t)stream));
+        return SM_OK;
+    }
+    // NULL: the default stream, which is what NULL means to every device entry point, and the
+    // handle's own stream (host entry points, FrameStream-style callers)
+    SM_HIP(hipStreamSynchronize(nullptr));
+    SM_HIP(hipStreamSynchronize(h->stream));
     return SM_OK;
 }
 

@@ -138,6 +138,8 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
     if keys_t.numel() != padded_pixels(H, W, world) or out_t.numel() != keys_t.numel():
         raise ValueError("keys_t / out_t must be dslice_buffers(H, W, world)")
     keys_img = keys_t[:P].view(H, W)
+    if stream is not None:   # frames and keys_t (last read by the previous collective) belong to the current stream
+        stream.wait_stream(torch.cuda.current_stream(left_t.device))
     if hi > lo:
         slice_keys(lo, hi, keys_img)
     else:
@@ -202,14 +204,20 @@ def band_rows(height: int, rank: int, world: int) -> Tuple[int, int]:
 MEDIAN_RADIUS = 3   # SM_MEDIAN: 7x7 post-filter (StereoDisparity.cpp:85)
 
 
+BAND_ALIGN = 32   # band inputs start on the frame's 32-row tile grid (sm_capi.hip group_bands)
+
+
 def band_halo(radius: int, agg: str = "box", median: bool = False) -> int:
-    """Input rows needed on each side of an output band: the aggregation window (2r for the
-    guided filter's two nested windows) plus the median's 3 rows when the post-filter is on."""
-    return (2 * radius if agg == "guided" else radius) + (MEDIAN_RADIUS if median else 0)
+    """Input rows needed on each side of an output band: the aggregation window (for the guided
+    filter's two nested windows 2r, at least 16 so that its 8-row float running sums of the kept
+    rows start on rows the band holds) plus the median's 3 rows when the post-filter is on."""
+    return (max(2 * radius, 16) if agg == "guided" else radius) + (MEDIAN_RADIUS if median else 0)
 
 
 def band_input_rows(height: int, y0: int, y1: int, halo: int) -> Tuple[int, int]:
-    return max(0, y0 - halo), min(height, y1 + halo)
+    """Input rows [ys, ye) of output band [y0, y1): ys floored to the 32-row tile grid."""
+    ys = 0 if y0 - halo <= 0 else ((y0 - halo) // BAND_ALIGN) * BAND_ALIGN
+    return ys, min(height, y1 + halo)
 
 
 def gather_bands(mine, height: int, world: int, group=None):
@@ -227,6 +235,8 @@ def band_disparity(matcher, left_t, right_t, radius: int, num_disp: int, y0: int
     import torch
     H = left_t.shape[-2]
     ys, ye = band_input_rows(H, y0, y1, band_halo(radius, agg, median))
+    if stream is not None:   # the frames were written on the current stream
+        stream.wait_stream(torch.cuda.current_stream(left_t.device))
     band = matcher.match_device(left_t[ys:ye], right_t[ys:ye], radius, num_disp, agg=agg, lr_check=lr_check,
                                 stream=stream, median=median)
     if stream is not None:

@@ -98,7 +98,9 @@ SM_API int sm_last_stage_ms(sm_handle *h, float *upload_ms, float *match_ms, flo
 /* ---- device-pointer entry points (inputs already resident in HBM) ----
  * All pointers are device pointers on the handle's device; `stream` is a hipStream_t used as
  * given (NULL = the device's default stream, as in the HIP runtime API).  Asynchronous: nothing
- * waits for completion.
+ * waits for completion.  Calls on one handle may use different streams: a pass that uses the
+ * handle's workspace (LR, median, staged, guided LR) first waits for the handle's previous pass
+ * when that ran on another stream.
  * `batch` frames are stored back to back: frame i starts at ptr + i*frame_stride. */
 SM_API int sm_match_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right,
                            int width, int height, int pitch, int batch, int64_t frame_stride,
@@ -130,7 +132,8 @@ SM_API int sm_guided_slice_keys_device(sm_handle *h, const uint8_t *d_left, cons
 SM_API int sm_guided_keys_to_disp_device(sm_handle *h, const int32_t *d_keys, int width, int height,
                                          uint8_t *d_disp, int out_pitch, void *stream);
 
-/* Wait for all work queued on `stream` (NULL = the handle's own stream). */
+/* Wait for all work queued on `stream`.  NULL means the default stream, as it does for every
+ * device entry point, and also waits for the handle's own stream. */
 SM_API int sm_stream_sync(sm_handle *h, void *stream);
 
 /* ---- caller-side steps in front of the path (SURVEY §8f "next") ----

@@ -231,30 +231,87 @@ def test_slice_keys_min_equals_full(matcher, oracle, torch, cuts):
 
 
 @pytest.mark.parametrize("G,agg,lr,med", [(2, "box", False, False), (8, "box", False, False), (3, "box", True, False),
-                                          (4, "guided", False, False), (5, "box", True, True), (3, "box", False, True)])
+                                          (4, "guided", False, False), (5, "box", True, True), (3, "box", False, True),
+                                          (3, "guided", True, True), (7, "guided", True, False)])
 def test_rowband_bands_equal_full_frame(matcher, torch, G, agg, lr, med):
     """The row-band partition's per-rank compute (sharding.band_disparity), run band by band on one
-    GPU, reassembles the single-pass map: bit-exact for box / LR, near-ties only for guided."""
+    GPU on its own stream, reassembles the single-pass map bit for bit, the guided filter included:
+    band inputs start on the frame's 32-row tile grid with a halo of max(2r, 16) (+3 with the
+    median), the C group's rule, so every kept row sees the full frame's summation order."""
     from gpu_stereo_matching_amd import sharding
     from oracle import oracle as O
     L, R = O.synth_pair(555, 700, 203, 64)
     Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
     full = matcher.match_device(Lt, Rt, 5, 64, agg=agg, lr_check=lr, median=med)
+    side = torch.cuda.Stream()
     parts = []
     for k in range(G):
         y0, y1 = sharding.band_rows(203, k, G)
         if y1 > y0:
-            parts.append(sharding.band_disparity(matcher, Lt, Rt, 5, 64, y0, y1, agg, lr, median=med))
+            parts.append(sharding.band_disparity(matcher, Lt, Rt, 5, 64, y0, y1, agg, lr, stream=side, median=med))
     got = torch.cat(parts)
     torch.cuda.synchronize()
-    if agg == "guided":
-        # band tiling changes the fp32 summation order: judged like the single pass, against fp64
-        from guided_check import tie_aware_check
-        disp_o, q, best = O.guided_disp(L, R, 5, 64, 1e-4 * 255 * 255, want_q=True)
-        ok, _ = tie_aware_check(got.cpu().numpy(), q, {"disp": disp_o, "best": best}, 64, L.shape[1])
-        assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
-    else:
-        assert torch.equal(got, full)
+    assert torch.equal(got, full)
+
+
+def test_null_stream_and_stream_sync(sm, matcher, oracle, torch):
+    """NULL means the default stream for sm_match_device AND for sm_stream_sync, so a C
+    caller that passes NULL to both reads a finished map."""
+    W, H, D, r = 640, 360, 128, 5
+    L, R = oracle.synth_pair(31, W, H, D)
+    want = oracle.box_disp(L, R, r, D)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    out = torch.full((H, W), 7, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    for flags in (sm.SM_AGG_BOX, sm.SM_AGG_BOX | sm.SM_LR_CHECK):
+        rc = matcher._lib.sm_match_device(matcher._h, Lt.data_ptr(), Rt.data_ptr(), W, H, W, 1, H * W, r, D, flags,
+                                          out.data_ptr(), W, H * W, None)
+        assert rc == 0
+        assert matcher._lib.sm_stream_sync(matcher._h, None) == 0
+        host = out.cpu().numpy()
+        if flags == sm.SM_AGG_BOX:
+            assert np.array_equal(host, want)
+        else:
+            assert np.array_equal(host, oracle.box_lr(L, R, r, D)[2])
+
+
+def test_two_streams_one_handle(matcher, oracle, torch):
+    """device calls on one handle from two streams share the handle's LR / median
+    workspace; the second pass waits for the first, so both maps are exact."""
+    W, H, D, r = 900, 400, 128, 5
+    pairs = [oracle.synth_pair(61 + i, W, H, D) for i in range(2)]
+    want = [oracle.box_lr(L, R, r, D)[2] for L, R in pairs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    dev = [(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()) for L, R in pairs]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        outs = [matcher.match_device(dev[0][0], dev[0][1], r, D, lr_check=True, median=True, stream=s1),
+                matcher.match_device(dev[1][0], dev[1][1], r, D, lr_check=True, median=True, stream=s2)]
+        torch.cuda.synchronize()
+        for o, (L, R) in zip(outs, pairs):
+            ref = matcher.match_lr(L, R, r, D, median=True)[0]
+            assert np.array_equal(o.cpu().numpy(), ref)
+    outs = [matcher.match_device(dev[i][0], dev[i][1], r, D, lr_check=True, stream=(s1, s2)[i]) for i in range(2)]
+    torch.cuda.synchronize()
+    for o, w in zip(outs, want):
+        assert np.array_equal(o.cpu().numpy(), w)
+
+
+def test_out_tensor_validation(matcher, torch):
+    """a caller-supplied output of the wrong shape / dtype / device is a ValueError, never
+    an out-of-bounds device write."""
+    Lt = torch.zeros((64, 96), dtype=torch.uint8, device="cuda")
+    for bad in (torch.empty((63, 96), dtype=torch.uint8, device="cuda"),
+                torch.empty((64, 96), dtype=torch.int32, device="cuda"),
+                torch.empty((64, 96), dtype=torch.uint8),
+                torch.empty((96, 64), dtype=torch.uint8, device="cuda").t()):
+        with pytest.raises(ValueError):
+            matcher.match_device(Lt, Lt, 2, 16, out_t=bad)
+    k = torch.zeros((64, 96), dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        matcher.keys_to_disp_device(k, 2, out_t=torch.empty((10,), dtype=torch.uint8, device="cuda"))
+    with pytest.raises(ValueError):
+        matcher.guided_keys_to_disp_device(k.float())
 
 
 def test_error_codes(sm, matcher):
