@@ -21,6 +21,7 @@ constexpr int kST = 256;
 constexpr int kSC = 4 * kST;       // K2: input columns per strip (4 per thread)
 constexpr int kSO = kSC - 16;      // K2: output columns per strip (the strip starts 8 columns early)
 constexpr int kSadBlocks = 4096;  // K2 blocks per launch (2048 measured 10 % slower, 8192 the same)
+constexpr int kSadRowsPerSync = 1; // K2 output rows staged in LDS per workgroup barrier (4 measured 2 % slower)
 
 // K2: one column strip x one row band of one d plane per block.  A thread owns 4 input columns
 // and walks the band's rows once: vertical window sums run in registers (two packed u16 pairs,
@@ -45,12 +46,16 @@ __device__ __forceinline__ uint32_t ld4z(const uint8_t* plane, int y, int x, int
 
 template <int R>
 __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict__ ad, int W, int H, int rows_per_band,
-                                                      uint16_t* __restrict__ sad) {
+                                                      int bands, int strips, uint16_t* __restrict__ sad) {
     constexpr int K = 2 * R + 1;
-    __shared__ __attribute__((aligned(16))) uint16_t vs[2][kSC + 16];
+    constexpr int RB = kSadRowsPerSync;
+    __shared__ __attribute__((aligned(16))) uint16_t vs[2][RB][kSC + 16];
     const int t = threadIdx.x;
-    const int sx = blockIdx.x, d = blockIdx.z;
-    const int yo0 = blockIdx.y * rows_per_band;
+    // XCD-aware order: each XCD walks a contiguous run of (plane, strip, band) ids, band fastest,
+    // so the 2r halo rows a band shares with the band above are still in that XCD's L2
+    const int id = xcd_tile(blockIdx.x, gridDim.x);
+    const int band = id % bands, sx = (id / bands) % strips, d = id / (bands * strips);
+    const int yo0 = band * rows_per_band;
     const int yo1 = min(H, yo0 + rows_per_band);
     if (yo0 >= H) return;                               // block-uniform
     const int64_t P = (int64_t)W * H;
@@ -59,12 +64,51 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
     const int xs = sx * kSO;                            // first output column of the strip
     const int xin = xs - 8 + 4 * t;                     // this thread's 4 input columns
     const bool vec_out = ((W & 3) == 0) && ((reinterpret_cast<uintptr_t>(sad) & 7) == 0);
+    const int x = xs + 4 * t;
+    const bool out_on = 4 * t < kSO && x < W;
     // vertical sums: E = (col0, col2), O = (col1, col3) as u16 pairs (<= (2r+1) * 255)
     uint32_t E = 0u, O = 0u, ring[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) ring[j] = 0u;
     const int yi_end = yo1 + R;                         // input rows [yo0 - R, yo1 + R)
-    int buf = 0;
+    int buf = 0, nrow = 0, yfirst = yo0;
+    // horizontal sums of the nrow rows staged in vs[buf] (rows yfirst ..), behind one barrier
+    auto flush = [&]() {
+        __syncthreads();
+        for (int q = 0; q < nrow; ++q) {
+            const uint16_t* row = vs[buf][q];
+            // outputs xs + 4t + k (k < 4): window of vs indices [4t + 8 + k - R, 4t + 8 + k + R]
+            uint32_t w[12];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+                const uint2 x2 = *reinterpret_cast<const uint2*>(row + 4 * t + 4 * u);
+                w[2 * u] = x2.x;
+                w[2 * u + 1] = x2.y;
+            }
+            auto val = [&](int i) -> uint32_t { return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu); };
+            uint32_t sum = 0;
+#pragma unroll
+            for (int i = 8 - R; i <= 8 + R; ++i) sum += val(i);
+            uint32_t res[4];
+            res[0] = sum;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                sum += val(8 + R + k) - val(8 - R + k - 1);
+                res[k] = sum;                           // <= (2r+1)^2 * 255 < 2^16 for r <= 7
+            }
+            if (out_on) {
+                uint16_t* dst = outp + (int64_t)(yfirst + q) * W + x;
+                if (vec_out && x + 4 <= W) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+                } else {
+                    for (int k = 0; k < 4 && x + k < W; ++k) dst[k] = (uint16_t)res[k];
+                }
+            }
+        }
+        buf ^= 1;                                       // the next rows go to the other buffer
+        yfirst += nrow;
+        nrow = 0;
+    };
     for (int base = yo0 - R; base < yi_end; base += K) {
         // ring slot j holds row base + j - K (this loop's row base + j replaces it)
         uint32_t nw[K];
@@ -78,47 +122,21 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
             ring[j] = v;
             E += (v & 0x00FF00FFu) - (o & 0x00FF00FFu);
             O += ((v >> 8) & 0x00FF00FFu) - ((o >> 8) & 0x00FF00FFu);
-            const int yo = yi - R;                      // window [yi - 2R, yi] is centred on yo
-            if (yo < yo0) continue;                     // warm-up rows of the band
-            uint16_t* row = vs[buf];
-            *reinterpret_cast<uint2*>(row + 4 * t) =
+            if (yi - R < yo0) continue;                 // warm-up rows of the band (window centred on yi - R)
+            *reinterpret_cast<uint2*>(&vs[buf][nrow][4 * t]) =
                 make_uint2(__builtin_amdgcn_perm(O, E, 0x05040100u), __builtin_amdgcn_perm(O, E, 0x07060302u));
-            __syncthreads();
-            // outputs xs + 4t + k (k < 4): window of vs indices [4t + 8 + k - R, 4t + 8 + k + R]
-            uint32_t w[12];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                const uint2 x2 = *reinterpret_cast<const uint2*>(row + 4 * t + 4 * q);
-                w[2 * q] = x2.x;
-                w[2 * q + 1] = x2.y;
-            }
-            auto val = [&](int i) -> uint32_t { return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu); };
-            uint32_t sum = 0;
-#pragma unroll
-            for (int i = 8 - R; i <= 8 + R; ++i) sum += val(i);
-            uint32_t res[4];
-            res[0] = sum;
-#pragma unroll
-            for (int k = 1; k < 4; ++k) {
-                sum += val(8 + R + k) - val(8 - R + k - 1);
-                res[k] = sum;                           // <= (2r+1)^2 * 255 < 2^16 for r <= 7
-            }
-            const int x = xs + 4 * t;
-            if (4 * t < kSO && x < W) {
-                uint16_t* dst = outp + (int64_t)yo * W + x;
-                if (vec_out && x + 4 <= W) {
-                    *reinterpret_cast<uint2*>(dst) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
-                } else {
-                    for (int k = 0; k < 4 && x + k < W; ++k) dst[k] = (uint16_t)res[k];
-                }
-            }
-            buf ^= 1;                                   // the next row's sums go to the other buffer
+            if (++nrow == RB) flush();
         }
     }
+    if (nrow) flush();
 }
 
 // K3: 8 pixels per thread, one 16-B nontemporal load per d plane (the volume is streamed once and
-// is larger than the MALL).
+// is larger than the MALL).  The loads of kWtaUnroll consecutive planes are issued before any of
+// them is used, so each wave keeps kWtaUnroll KB in flight (one plane at a time measured 4.4 TB/s:
+// a read stream needs ~20 KB in flight per CU at HBM latency).
+constexpr int kWtaUnroll = 8;
+
 __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restrict__ sad, int W, int H, int D,
                                                          uint32_t seed_key, uint8_t* __restrict__ disp,
                                                          int out_pitch) {
@@ -134,25 +152,41 @@ __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restr
         lim[k] = W - (int)((p0 + k) % W);            // validity: d <= W - x (Device.cu:44)
         best[k] = seed_key;
     }
+    auto take = [&](uint32_t word, int k, int d) {
+        const uint32_t key = (word << 8) | (uint32_t)d;
+        best[k] = (d <= lim[k] && key < best[k]) ? key : best[k];
+    };
     const bool vec = n == NPX && ((reinterpret_cast<uintptr_t>(sad) & 15) == 0) && ((P & 7) == 0);
-    for (int d = 0; d < D; ++d) {
-        const uint16_t* pl = sad + (int64_t)d * P + p0;
-        uint32_t s[NPX];
-        if (vec) {
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pl));
+    if (vec) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(sad + p0);
+        const int64_t pstride = P / 8;                // one plane in u32x4 units
+        int d = 0;
+        for (; d + kWtaUnroll <= D; d += kWtaUnroll) {
+            u32x4 v[kWtaUnroll];
+#pragma unroll
+            for (int u = 0; u < kWtaUnroll; ++u) v[u] = __builtin_nontemporal_load(base + (int64_t)(d + u) * pstride);
+#pragma unroll
+            for (int u = 0; u < kWtaUnroll; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    take(v[u][q] & 0xFFFFu, 2 * q, d + u);
+                    take(v[u][q] >> 16, 2 * q + 1, d + u);
+                }
+        }
+        for (; d < D; ++d) {
+            const u32x4 v = __builtin_nontemporal_load(base + (int64_t)d * pstride);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                s[2 * q] = v[q] & 0xFFFFu;
-                s[2 * q + 1] = v[q] >> 16;
+                take(v[q] & 0xFFFFu, 2 * q, d);
+                take(v[q] >> 16, 2 * q + 1, d);
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < NPX; ++k) s[k] = k < n ? pl[k] : 0u;
         }
+    } else {
+        for (int d = 0; d < D; ++d) {
+            const uint16_t* pl = sad + (int64_t)d * P + p0;
 #pragma unroll
-        for (int k = 0; k < NPX; ++k) {
-            const uint32_t key = (s[k] << 8) | (uint32_t)d;
-            best[k] = (d <= lim[k] && key < best[k]) ? key : best[k];
+            for (int k = 0; k < NPX; ++k)
+                if (k < n) take(pl[k], k, d);
         }
     }
 #pragma unroll
@@ -173,8 +207,9 @@ hipError_t launch_box_sad_r(const uint8_t* ad, int W, int H, int D, uint16_t* sa
     bands = bands < 1 ? 1 : (bands > max_bands ? max_bands : bands);
     const int rows = (H + bands - 1) / bands;
     bands = (H + rows - 1) / rows;
-    if (D > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(box_sad_kernel<R>, dim3(strips, bands, D), dim3(kST), 0, s, ad, W, H, rows, sad);
+    const int64_t blocks = (int64_t)strips * bands * D;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(box_sad_kernel<R>, dim3((unsigned)blocks), dim3(kST), 0, s, ad, W, H, rows, bands, strips, sad);
     return hipGetLastError();
 }
 
