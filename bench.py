@@ -35,6 +35,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction issues over 2 cycles per SIMD (32 lanes
+# per cycle, MI355X_MICROARCH.md "Execution model"), 2.4 GHz engine clock: 78.64 T lane-ops/s.  Measured
+# on this part (profiles/microbench/r02_valu_issue_*.txt): add/sub/mul/fma/shift 2.4 cycles per
+# wave-instruction, sad/perm/min/mul24/3-operand integer ops 4.2, cvt 7.7.
+VALU_PEAK_TLANEOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+CU_CLOCK_HZ = 2.4e9
 
 
 def parse():
@@ -56,6 +62,7 @@ def parse():
     ap.add_argument("--profile", action="store_true",
                     help="only the timed steps (what rocprof summaries under profiles/ are taken from)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_box_r5_1080p.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_counts.json"))
     return ap.parse_args()
 
 
@@ -63,6 +70,36 @@ def algorithmic_bytes_per_map(W: int, H: int, D: int) -> int:
     """the reference data flow moves B = P*(2D+3) bytes per map
     (L+R in, the D-plane uint8 AD volume written once and read once, disparity out)."""
     return W * H * (2 * D + 3)
+
+
+def load_counts(path):
+    try:
+        with open(path) as f:
+            return json.load(f).get("kernels", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None):
+    """roofline on the binding resource of a compute-bound kernel: VALU lane-ops per second, from
+    SQ_INSTS_VALU per launch (profiles/valu_counts.json, tools/valu_counts.py, same workload) over
+    the live launch time; LDS-array busy fraction from SQ_LDS_IDX_ACTIVE beside it."""
+    c = counts.get(key)
+    if not c or c.get("workload") != list(workload):
+        return {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TLANEOPS, 2), "unit": "T lane-op/s",
+                "frac": None, "kernel": kernel, "note": f"no SQ_INSTS_VALU count for {key} in profiles/valu_counts.json"}
+    pl = c["per_launch"]
+    t = launch_ms * 1e-3
+    achieved = pl["SQ_INSTS_VALU"] * 64 / t / 1e12
+    res = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TLANEOPS, 2),
+           "unit": "T lane-op/s", "frac": round(achieved / VALU_PEAK_TLANEOPS, 4), "kernel": kernel,
+           "kernel_ms_per_launch": round(launch_ms, 5), "valu_wave_insts_per_launch": pl["SQ_INSTS_VALU"],
+           "lds_busy_frac": round(pl["SQ_LDS_IDX_ACTIVE"] / (256 * t * CU_CLOCK_HZ), 4)
+           if "SQ_LDS_IDX_ACTIVE" in pl else None,
+           "counts_source": "profiles/valu_counts.json (rocprofv3 --pmc SQ_INSTS_VALU, tools/valu_counts.py)"}
+    if extra:
+        res.update(extra)
+    return res
 
 
 def cpu_baseline(W, H, D, r, seed):
@@ -169,6 +206,21 @@ def run_variants(sm, torch, dev, stream, seed):
         out["staged box 1080p 11x11 d128 (AD u8 -> SAD u16 -> WTA through HBM, HBM-bound)"] = {
             "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "achieved_GBs": round(gbs, 1),
             "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 3), "bytes_per_frame": nbytes}
+        # per kernel: HIP events around each kernel of one staged frame (sm_last_staged_kernel_ms), median of 10
+        P = W * H
+        per = {}
+        kt = []
+        for _ in range(10):
+            m.match_device(Lt, Rt, 5, D, out_t=o1, agg="box-staged", stream=stream)
+            kt.append(m.staged_kernel_ms())
+        kt = np.median(np.array(kt), axis=0)
+        for kname, kms, nb in (("ad_volume_kernel", float(kt[0]), P * (D + 2)),
+                               ("box_sad_kernel", float(kt[1]), 3 * P * D),
+                               ("volume_wta_kernel", float(kt[2]), 2 * P * D + P)):
+            g_ = nb / (kms * 1e-3) / 1e9
+            per[kname] = {"ms": round(kms, 4), "algorithmic_bytes": nb, "achieved_GBs": round(g_, 1),
+                          "frac_of_hbm_peak": round(g_ / HBM_PEAK_GBS, 3)}
+        out["staged kernels 1080p d128 (HBM roofline per kernel)"] = per
         # host frame stream, PCIe-inclusive: FrameStream overlaps H2D / match / D2H on three streams;
         # frames are produced in place in the pinned slots (next_inputs) and consumed in place
         # (callback), so no host-side copy is timed
@@ -423,7 +475,7 @@ def main():
 
     if rank == 0:
         bpm = algorithmic_bytes_per_map(W, H, D)
-        achieved = bpm * B / (kern_ms * 1e-3) / 1e9
+        eq_hbm = bpm * B / (kern_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(args.pmc_json) as f:
@@ -432,7 +484,16 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-
+        counts = load_counts(args.valu_json)
+        roof = valu_roofline(counts, "box_r5_1080p_d128_b32", [W, H, D, r, B], kern_ms, f"box_match_kernel<{r}>", {
+            "traffic": traffic,
+            "traffic_frac_of_hbm_peak": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "equivalent_hbm_frac": round(eq_hbm / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch": bpm * B,
+            "note": "bound = VALU issue (the fused kernel reads the pair and writes the map: measured HBM traffic is "
+                    "the compulsory 3P bytes, traffic_frac_of_hbm_peak); equivalent_hbm_frac = P*(2D+3) bytes per "
+                    "map (SURVEY §8d, the reference's AD-volume data flow, never materialised here) / launch time / "
+                    "8 TB/s: a speed figure, not a roofline fraction (DESIGN.md §8)"})
         res = {
             "metric": "disparity-maps/sec + ms/frame, 1080p d_max=128",
             "value": round(value, 2),
@@ -456,15 +517,7 @@ def main():
                 "width": W, "height": H, "num_disp": D, "radius": r, "frames_per_step_per_gpu": B,
                 "seed": args.seed, "parallelism": f"frame-parallel x{world}",
             },
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"box_match_kernel<{r}>", "kernel_ms_per_launch": round(kern_ms, 5),
-                "algorithmic_bytes_per_launch": bpm * B,
-                "note": "algorithmic bytes = P*(2D+3) per map (SURVEY §8d, the reference's AD-volume data flow); "
-                        "the fused kernel never writes that volume, so frac > 1 is possible and the kernel is "
-                        "VALU/LDS-bound (DESIGN.md §Roofline)",
-            },
+            "roofline": roof,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
         }
@@ -487,14 +540,18 @@ def main():
                                       "with_lr_check": {"value": glr.get("maps_per_s"),
                                                         "ms_per_frame": glr.get("ms_per_frame")},
                                       "kernel": "guided_fused_kernel<5>", "dtype": "fp32 (u8 in/out)"}
-                # the same algorithmic-bytes roofline as the headline (P*(2D+3) per map); the guided
-                # kernel reads only the pair and writes the map, and is VALU/LDS-bound
-                ga = bpm / (g["ms_per_frame"] * 1e-3) / 1e9
-                res["cfg3_guided"]["roofline"] = {
-                    "bound": "hbm", "achieved": round(ga, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ga / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_map": bpm,
-                    "note": "compute-bound in fact: ~60-70 % VALU and ~60 % LDS busy per PMC "
-                            "(profiles/pmc_guided_counters_r5_1080p.json)"}
+                res["cfg3_guided"]["roofline"] = valu_roofline(
+                    counts, "guided_r5_1080p_d128_b32", [1920, 1080, 128, 5, g["frames_per_call"]],
+                    g["ms_per_frame"] * g["frames_per_call"], "guided_fused_kernel<5, false>",
+                    {"equivalent_hbm_frac": round(bpm / (g["ms_per_frame"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+                if "maps_per_s" in glr:
+                    res["cfg3_guided"]["with_lr_check"]["roofline"] = valu_roofline(
+                        counts, "guided_lr_r5_1080p_d128_b32", [1920, 1080, 128, 5, glr["frames_per_call"]],
+                        glr["ms_per_frame"] * glr["frames_per_call"], "guided_fused_kernel<5, true> (+ right-key "
+                        "reduction and LR check in the launch time)")
+            st = variants.get("staged kernels 1080p d128 (HBM roofline per kernel)")
+            if st:
+                res["staged_hbm_roofline"] = st
         print(json.dumps(res), flush=True)
 
     m.close()

@@ -30,6 +30,7 @@ SM_PARAM_GUIDED_EPS = 1
 EXPORTED = (
     "sm_version", "sm_last_error_string", "sm_device_count", "sm_create", "sm_destroy",
     "sm_set_param_f", "sm_block_match_u8", "sm_block_match_lr_u8", "sm_last_stage_ms",
+    "sm_last_staged_kernel_ms",
     "sm_match_device", "sm_slice_keys_device", "sm_keys_to_disp_device", "sm_stream_sync",
     "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8", "sm_median_u8_device",
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
@@ -78,6 +79,7 @@ def load(path: str = LIB_PATH):
     L.sm_block_match_lr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, vp, vp, i]
     L.sm_last_stage_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                    ctypes.POINTER(ctypes.c_float)]
+    L.sm_last_staged_kernel_ms.argtypes = L.sm_last_stage_ms.argtypes
     L.sm_match_device.argtypes = [vp, vp, vp, i, i, i, i, i64, i, i, u, vp, i, i64, vp]
     L.sm_slice_keys_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp, vp]
     L.sm_keys_to_disp_device.argtypes = [vp, vp, i, i, i, vp, i, vp]

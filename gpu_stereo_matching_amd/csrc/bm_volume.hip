@@ -16,6 +16,15 @@ namespace sm {
 namespace {
 
 constexpr int kVT = 256;
+#ifndef SM_ADV_BLOCKS
+#define SM_ADV_BLOCKS 4096
+#endif
+#ifndef SM_ADV_MAXSPLIT
+#define SM_ADV_MAXSPLIT 16
+#endif
+#ifndef SM_ADV_NT
+#define SM_ADV_NT 1
+#endif
 constexpr int kVPad = 16;   // zero bytes in front of the staged R row (x - d down to -15)
 
 typedef short v2i16 __attribute__((ext_vector_type(2)));
@@ -112,7 +121,8 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
         if (vec) {
             // streaming output (P*D bytes, larger than the MALL): nontemporal 16-B stores
             const u32x4 v = {o[0], o[1], o[2], o[3]};
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+            if (SM_ADV_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+            else *reinterpret_cast<u32x4*>(dst) = v;
         } else {
             const int n = W - x0 < 16 ? W - x0 : 16;
             for (int b = 0; b < n; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
@@ -128,8 +138,8 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     if (W <= 0 || H <= 0 || D <= 0 || batch <= 0 || nseg > kVT) return hipErrorInvalidValue;
     const size_t lds = (size_t)(kVPad + nseg * 16 + 4 + 15) & ~(size_t)15;
     // enough blocks in flight (>= ~4 per CU of 256) to keep the stores streaming
-    int dsplit = (4096 + H * batch - 1) / (H * batch);
-    dsplit = dsplit < 1 ? 1 : (dsplit > D ? D : (dsplit > 16 ? 16 : dsplit));
+    int dsplit = (SM_ADV_BLOCKS + H * batch - 1) / (H * batch);
+    dsplit = dsplit < 1 ? 1 : (dsplit > D ? D : (dsplit > SM_ADV_MAXSPLIT ? SM_ADV_MAXSPLIT : dsplit));
     hipLaunchKernelGGL(ad_volume_kernel, dim3(H, batch, dsplit), dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D,
                        dif, dstride);
     return hipGetLastError();

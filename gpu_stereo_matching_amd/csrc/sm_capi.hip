@@ -58,6 +58,9 @@ struct sm_handle {
     bool scratch_pending = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float stage_ms[3] = {0.f, 0.f, 0.f};
+    // staged box path: events around the last frame's AD / SAD / WTA kernels (sm_last_staged_kernel_ms)
+    hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool kev_valid = false;
 };
 
 namespace {
@@ -167,13 +170,22 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     uint8_t* ad = h->d_vol;
     uint16_t* sad = reinterpret_cast<uint16_t*>(h->d_vol + P * D);
     uint8_t* raw = h->d_vol + 3 * P * D;
+    if (!h->kev[0])
+        for (auto& e : h->kev) SM_HIP(hipEventCreate(&e));
+    h->kev_valid = false;
     for (int f = 0; f < batch; ++f) {
+        const bool last = f == batch - 1;   // the last frame's kernels are bracketed by events
+        if (last) SM_HIP(hipEventRecord(h->kev[0], s));
         SM_HIP(sm::launch_ad_volume(L + f * fstride, R + f * fstride, W, H, pitch, fstride, 1, D, ad, P * D, s));
+        if (last) SM_HIP(hipEventRecord(h->kev[1], s));
         SM_HIP(sm::launch_box_sad_volume(ad, W, H, radius, D, sad, s));
+        if (last) SM_HIP(hipEventRecord(h->kev[2], s));
         uint8_t* out = disp + f * ostride;
         SM_HIP(sm::launch_volume_wta(sad, W, H, D, seed_key(radius), med ? raw : out, med ? W : opitch, s));
+        if (last) SM_HIP(hipEventRecord(h->kev[3], s));
         if (med) SM_HIP(sm::launch_median(raw, W, H, W, P, 1, 3, out, opitch, ostride, s));
     }
+    h->kev_valid = batch > 0;
     return SM_OK;
 }
 
@@ -543,6 +555,8 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_bgr);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : h->kev)
+        if (ev) (void)hipEventDestroy(ev);
     if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -570,6 +584,18 @@ SM_API int sm_block_match_lr_u8(sm_handle* h, const uint8_t* left, const uint8_t
                                 uint8_t* right_disp_out, uint8_t* valid_mask_out, int out_pitch) {
     return host_match(h, left, right, width, height, pitch, radius, num_disp, flags | SM_LR_CHECK, disp_out,
                       right_disp_out, valid_mask_out, out_pitch);
+}
+
+SM_API int sm_last_staged_kernel_ms(sm_handle* h, float* ad_ms, float* sad_ms, float* wta_ms) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!h->kev_valid) return fail(SM_ERR_INVALID_ARG, "no SM_STAGED pass has run on this handle");
+    SM_HIP(hipEventSynchronize(h->kev[3]));
+    float t[3];
+    for (int i = 0; i < 3; ++i) SM_HIP(hipEventElapsedTime(&t[i], h->kev[i], h->kev[i + 1]));
+    if (ad_ms) *ad_ms = t[0];
+    if (sad_ms) *sad_ms = t[1];
+    if (wta_ms) *wta_ms = t[2];
+    return SM_OK;
 }
 
 SM_API int sm_last_stage_ms(sm_handle* h, float* upload_ms, float* match_ms, float* download_ms) {

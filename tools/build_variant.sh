@@ -1,0 +1,19 @@
+#!/bin/bash
+# Build a libsm_hip.so variant for same-box A/B timing: tools/build_variant.sh NAME "-DFOO=1 ..."
+# -> tools/ab/NAME.so (objects under tools/ab/NAME/).  Not part of the product build.
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; shift
+EXTRA="$*"
+SRC=gpu_stereo_matching_amd/csrc
+OUT=tools/ab/$NAME
+mkdir -p $OUT
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wall -Wno-unused-result $EXTRA"
+pids=()
+for f in sm_capi bm_box bm_aux bm_guided bm_pre bm_post bm_volume bm_staged bm_rectify; do
+  /opt/rocm/bin/hipcc $FLAGS -c $SRC/$f.hip -o $OUT/$f.o &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p; done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ab/$NAME.so $OUT/*.o
+echo built tools/ab/$NAME.so

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -32,6 +33,33 @@ __global__ __launch_bounds__(256) void wr(u32x4* __restrict__ p, size_t n) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         if (NT) __builtin_nontemporal_store(v, p + i);
         else p[i] = v;
+    }
+}
+
+// one dword (or 8 B) per lane, grid-stride (256 B / 512 B per wave-instruction)
+template <class T, bool NT>
+__global__ __launch_bounds__(256) void wrw(T* __restrict__ p, size_t n) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    T v;
+    __builtin_memset(&v, (int)threadIdx.x, sizeof(T));
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        if (NT) __builtin_nontemporal_store(v, p + i);
+        else p[i] = v;
+    }
+}
+
+// each workgroup writes one contiguous chunk of CH 16-B vectors per lane (no grid stride)
+template <int CH, bool NT>
+__global__ __launch_bounds__(256) void wrc(u32x4* __restrict__ p, size_t n) {
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1, 2};
+    const size_t base = (size_t)blockIdx.x * 256 * CH + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const size_t i = base + (size_t)k * 256;
+        if (i < n) {
+            if (NT) __builtin_nontemporal_store(v, p + i);
+            else p[i] = v;
+        }
     }
 }
 
@@ -75,6 +103,25 @@ int main() {
     (void)hipMalloc(&o, 64);
     (void)hipMemset(a, 1, bytes);
     (void)hipMemset(b, 2, bytes);
+    if (getenv("HBM_WRITE_ONLY")) {
+        for (int blocks : {2048, 8192, 32768}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "write 4B plain, %d blocks", blocks);
+            timeit(nm, bytes, [&] { wrw<uint32_t, false><<<blocks, 256>>>((uint32_t*)b, bytes / 4); });
+            snprintf(nm, sizeof nm, "write 4B nt, %d blocks", blocks);
+            timeit(nm, bytes, [&] { wrw<uint32_t, true><<<blocks, 256>>>((uint32_t*)b, bytes / 4); });
+            snprintf(nm, sizeof nm, "write 8B plain, %d blocks", blocks);
+            timeit(nm, bytes, [&] { wrw<uint64_t, false><<<blocks, 256>>>((uint64_t*)b, bytes / 8); });
+            snprintf(nm, sizeof nm, "write 16B plain, %d blocks", blocks);
+            timeit(nm, bytes, [&] { wr<false><<<blocks, 256>>>(b, n); });
+        }
+        timeit("write 16B chunk 16/lane plain", bytes, [&] { wrc<16, false><<<(unsigned)(n / (256 * 16)), 256>>>(b, n); });
+        timeit("write 16B chunk 16/lane nt", bytes, [&] { wrc<16, true><<<(unsigned)(n / (256 * 16)), 256>>>(b, n); });
+        timeit("write 16B chunk 4/lane plain", bytes, [&] { wrc<4, false><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        timeit("write 16B chunk 4/lane nt", bytes, [&] { wrc<4, true><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        timeit("write 16B chunk 1/lane plain", bytes, [&] { wrc<1, false><<<(unsigned)(n / 256), 256>>>(b, n); });
+        return 0;
+    }
     for (int blocks : {1024, 2048, 4096, 8192}) {
         char nm[64];
         snprintf(nm, sizeof nm, "read 16B x4 unroll, %d blocks", blocks);

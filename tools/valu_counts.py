@@ -1,0 +1,49 @@
+"""VALU / LDS instruction counts per launch of the bench's compute-bound kernels, for bench.py's
+`roofline` (bound "valu").  One rocprofv3 --pmc pass per workload (SQ counters only, no tracing
+domains: MI355X_MICROARCH.md §PMC), on tools/kernel_driver.py with the bench's exact configuration
+(1080p D=128 r=5, 32 frames per launch).  SQ_INSTS_VALU is a chip total of wave64 instructions and
+does not depend on timing, so bench.py divides it by the live HIP-event kernel time.
+
+    python tools/valu_counts.py            # writes profiles/valu_counts.json
+"""
+import csv, glob, json, os, statistics, subprocess, sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CTRS = "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
+# name, kernel-name substring, driver args; workload = [W, H, D, r, frames per launch]
+JOBS = (
+    ("box_r5_1080p_d128_b32", "box_match_kernel<5, 128, false>", ["--agg", "box", "--batch", "32"], [1920, 1080, 128, 5, 32]),
+    ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false>", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
+    ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true>", ["--agg", "guided", "--lr", "--batch", "32"],
+     [1920, 1080, 128, 5, 32]),
+)
+
+
+def main():
+    env = dict(os.environ, TMPDIR="/tmp")
+    tag = os.environ.get("SM_TAG", "")
+    res = {"counters": CTRS.split(), "note": "chip totals per launch (median over launches); SQ_INSTS_VALU counts "
+           "wave64 VALU instructions, SQ_LDS_IDX_ACTIVE LDS-array cycles summed over CUs", "kernels": {}}
+    for name, kname, args, wl in JOBS:
+        d = os.path.join(ROOT, "gpurun_out", "valu_counts" + tag, name)
+        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc"] + CTRS.split() + [
+            "-d", d, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
+            os.path.join(ROOT, "tools", "kernel_driver.py"), "--iters", "3"] + args
+        if os.environ.get("SM_LIB"):
+            cmd += ["--lib", os.environ["SM_LIB"]]
+        subprocess.run(cmd, check=True, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        vals = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if kname in row["Kernel_Name"]:
+                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        med = {k: statistics.median(v) for k, v in vals.items()}
+        res["kernels"][name] = {"kernel": kname, "workload": wl, "per_launch": med}
+        print(name, json.dumps(med), flush=True)
+    out = os.path.join(ROOT, "gpurun_out", "valu_counts%s.json" % tag)
+    json.dump(res, open(out, "w"), indent=1)
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    main()
