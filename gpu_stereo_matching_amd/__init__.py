@@ -109,14 +109,18 @@ class BlockMatcher:
 
     # -- host-pointer path (blockMatching_gpu replacement) -------------------------------
     def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
-              median: bool = False) -> np.ndarray:
-        """median=True: 7x7 median of the WTA map(s) (STMatching MeanFilter(disp, disp, 3)), before the LR check."""
+              median: bool = False, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """median=True: 7x7 median of the WTA map(s) (STMatching MeanFilter(disp, disp, 3)), before the LR check.
+        out: optional contiguous uint8 [H, W] host buffer (e.g. pinned memory) to write the map into."""
         L = _as_u8_image(left, "left")
         R = _as_u8_image(right, "right")
         if L.shape != R.shape:
             raise ValueError("left/right sizes differ")
         H, W = L.shape
-        out = np.empty((H, W), np.uint8)
+        if out is None:
+            out = np.empty((H, W), np.uint8)
+        elif out.dtype != np.uint8 or out.shape != (H, W) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint8 array of the frame's shape")
         _capi.check(self._lib.sm_block_match_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
                                                 _flags(agg, lr_check, median), out.ctypes.data, W))
         return out
@@ -421,6 +425,22 @@ class BlockMatcherGroup:
                                                          num_disp, _flags(agg, True, median), out.ctypes.data,
                                                          rd.ctypes.data, mask.ctypes.data, W))
         return out, rd, mask
+
+    def match_dslice(self, left, right, radius: int, num_disp: int, agg: str = "box") -> np.ndarray:
+        """One frame sharded over disparities (sm_group_dslice_block_match_u8): each member matches
+        its slice of [0, num_disp), RCCL MIN reduce-scatter + all-gather over the members' devices.
+        Members must be distinct devices."""
+        if agg not in ("box", "guided"):
+            raise ValueError("agg must be 'box' or 'guided'")
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        if L.shape != R.shape:
+            raise ValueError("left/right sizes differ")
+        H, W = L.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_group_dslice_block_match_u8(self._g, L.ctypes.data, R.ctypes.data, W, H, W, radius,
+                                                             num_disp, _flags(agg, False, False), out.ctypes.data, W))
+        return out
 
     def match_batch(self, lefts, rights, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
                     median: bool = False):

@@ -36,7 +36,7 @@ EXPORTED = (
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
     "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
-    "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_guided_slice_keys_device",
+    "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
     "sm_guided_keys_to_disp_device",
 )
 
@@ -105,6 +105,7 @@ def load(path: str = LIB_PATH):
     L.sm_group_block_match_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, i]
     L.sm_group_block_match_lr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, vp, vp, i]
     L.sm_group_block_match_batch_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
+    L.sm_group_dslice_block_match_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, i]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

@@ -7,7 +7,9 @@
 //   * every HIP call is checked and surfaced as an int status + sm_last_error_string()
 //     (the reference never checks, so its W > 1024 launch failure returns all zeros, :253);
 //   * any frame size works (the reference's fixed (8,10,D)x(32,32) grid covers 320x256 only, :231-233).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <cstdio>
 #include <cstring>
 #include <condition_variable>
@@ -58,6 +60,10 @@ struct sm_handle {
     bool scratch_pending = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float stage_ms[3] = {0.f, 0.f, 0.f};
+    // RCCL d-slice group mode (sm_group_dslice_block_match_u8): slice keys, this member's reduced
+    // key chunk, its uint8 chunk and the gathered map (grown on demand)
+    uint8_t* d_dsl = nullptr;
+    size_t dsl_bytes = 0;
     // staged box path: events around the last frame's AD / SAD / WTA kernels (sm_last_staged_kernel_ms)
     hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool kev_valid = false;
@@ -416,6 +422,8 @@ struct GroupWorker {
 
 struct sm_group {
     std::vector<GroupWorker*> w;
+    // one RCCL communicator per member for the d-slice mode, created on first use (ncclCommInitAll)
+    std::vector<ncclComm_t> comms;
 };
 
 namespace {
@@ -444,6 +452,128 @@ int group_run(sm_group* g, std::vector<std::function<int()>>& jobs) {
         }
     }
     if (rc) return fail(rc, "%s", err.c_str());
+    return SM_OK;
+}
+
+// RCCL is loaded on first use of the d-slice mode, not linked: callers that never shard a frame over
+// disparities carry no RCCL dependency.  The soname matches the copy PyTorch-ROCm ships, so inside a
+// torch process dlopen returns the already-loaded library (one RCCL per process).
+struct RcclApi {
+    decltype(&ncclCommInitAll) init_all;
+    decltype(&ncclCommDestroy) destroy;
+    decltype(&ncclReduceScatter) reduce_scatter;
+    decltype(&ncclAllGather) all_gather;
+    decltype(&ncclGetErrorString) error_string;
+};
+
+const RcclApi* rccl_api() {
+    static std::mutex mu;
+    static RcclApi api;
+    static int state = 0;   // 0 untried, 1 loaded, -1 unavailable
+    std::lock_guard<std::mutex> lk(mu);
+    if (state == 0) {
+        void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        state = -1;
+        if (lib) {
+            api.init_all = reinterpret_cast<decltype(api.init_all)>(dlsym(lib, "ncclCommInitAll"));
+            api.destroy = reinterpret_cast<decltype(api.destroy)>(dlsym(lib, "ncclCommDestroy"));
+            api.reduce_scatter = reinterpret_cast<decltype(api.reduce_scatter)>(dlsym(lib, "ncclReduceScatter"));
+            api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(lib, "ncclAllGather"));
+            api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(lib, "ncclGetErrorString"));
+            if (api.init_all && api.destroy && api.reduce_scatter && api.all_gather && api.error_string) state = 1;
+        }
+    }
+    return state == 1 ? &api : nullptr;
+}
+
+#define SM_RCCL(api, call)                                                                         \
+    do {                                                                                           \
+        ncclResult_t r_ = (call);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return fail(SM_ERR_LAUNCH, "%s failed: %s (%s:%d)", #call, (api)->error_string(r_), __FILE__, \
+                        __LINE__);                                                                 \
+    } while (0)
+
+int group_comms(sm_group* g) {
+    if (!g->comms.empty()) return SM_OK;
+    const RcclApi* api = rccl_api();
+    if (!api) return fail(SM_ERR_DEVICE, "d-slice mode: librccl.so.1 not loadable (%s)", dlerror());
+    const int n = (int)g->w.size();
+    std::vector<int> devs(n);
+    for (int k = 0; k < n; ++k) {
+        devs[k] = g->w[k]->h->device;
+        for (int j = 0; j < k; ++j)
+            if (devs[j] == devs[k])
+                return fail(SM_ERR_INVALID_ARG, "d-slice mode needs distinct devices (device %d twice)", devs[k]);
+    }
+    std::vector<ncclComm_t> comms(n, nullptr);
+    SM_RCCL(api, api->init_all(comms.data(), n, devs.data()));
+    g->comms = comms;
+    return SM_OK;
+}
+
+// One member's share of a d-sliced frame (runs on that member's worker thread): upload the pair,
+// slice keys over [lo, hi), MIN reduce-scatter of the int32 keys, finalise this member's pixel
+// chunk to uint8, all-gather the chunks; member 0 downloads the map.
+int dslice_member(sm_handle* h, ncclComm_t comm, int k, int n, const uint8_t* left, const uint8_t* right, int W,
+                  int H, int pitch, int radius, int D, bool guided, uint8_t* disp_out, int out_pitch) {
+    const RcclApi* api = rccl_api();
+    const int64_t P = (int64_t)W * H;
+    const int64_t chunk = (P + n - 1) / n, Ppad = chunk * n;
+    const size_t need = (size_t)(Ppad * 4 + chunk * 4 + chunk + Ppad);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    if (h->dsl_bytes < need) {
+        if (h->d_dsl) (void)hipFree(h->d_dsl);
+        h->d_dsl = nullptr;
+        h->dsl_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_dsl, need));
+        h->dsl_bytes = need;
+    }
+    uint32_t* keys = reinterpret_cast<uint32_t*>(h->d_dsl);
+    uint32_t* mine = keys + Ppad;
+    uint8_t* mine8 = reinterpret_cast<uint8_t*>(mine + chunk);
+    uint8_t* map = mine8 + chunk;
+    SM_HIP(copy2d(h->d_left, W, left, pitch, W, H, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, W, right, pitch, W, H, hipMemcpyHostToDevice, s));
+    // keys no d of the slice improves: the Device.cu:37 seed (box) / INT32_MAX (guided, signed keys)
+    const uint32_t none = guided ? 0x7FFFFFFFu : seed_key(radius);
+    const int lo = (int)((int64_t)k * D / n), hi = (int)((int64_t)(k + 1) * D / n);
+    if (Ppad > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(Ppad - P), s));
+    if (hi > lo) {
+        if (guided) {
+            SM_HIP(sm::launch_guided_slice_keys(h->d_left, h->d_right, W, H, W, 1, P, radius, lo, hi, h->guided_eps,
+                                                reinterpret_cast<int*>(keys), s));
+        } else {
+            sm::MatchArgs a{};
+            a.left = h->d_left;
+            a.right = h->d_right;
+            a.W = W;
+            a.H = H;
+            a.pitch = W;
+            a.frame_stride = P;
+            a.radius = radius;
+            a.d_lo = lo;
+            a.d_hi = hi;
+            a.valid_mode = 0;
+            a.seed_key = seed_key(radius);
+            a.thresh_key = seed_key(radius);
+            a.keys = keys;
+            SM_HIP(sm::launch_box_match(a, 1, s));
+        }
+    } else {
+        SM_HIP(hipMemsetD32Async(keys, (int)none, (size_t)P, s));
+    }
+    // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
+    SM_RCCL(api, api->reduce_scatter(keys, mine, (size_t)chunk, guided ? ncclInt32 : ncclUint32, ncclMin, comm, s));
+    if (guided)
+        SM_HIP(sm::launch_guided_keys_to_disp(reinterpret_cast<const int*>(mine), (int)chunk, 1, mine8, (int)chunk, s));
+    else
+        SM_HIP(sm::launch_keys_to_disp(mine, (int)chunk, 1, seed_key(radius), mine8, (int)chunk, s));
+    SM_RCCL(api, api->all_gather(mine8, map, (size_t)chunk, ncclUint8, comm, s));
+    if (k == 0) SM_HIP(copy2d(disp_out, out_pitch, map, W, W, H, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
 }
 
@@ -553,6 +683,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipFree(h->d_maps);
     (void)hipFree(h->d_vol);
     (void)hipFree(h->d_bgr);
+    (void)hipFree(h->d_dsl);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : h->kev)
@@ -570,6 +701,7 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
         h->guided_eps = value;
         return SM_OK;
     }
+
     return fail(SM_ERR_INVALID_ARG, "unknown param %d", param);
 }
 
@@ -985,6 +1117,11 @@ SM_API int sm_create_group(int ngpu, const int* devices, int max_width, int max_
 
 SM_API int sm_destroy_group(sm_group* g) {
     if (!g) return SM_OK;
+    if (!g->comms.empty()) {
+        const RcclApi* api = rccl_api();
+        for (ncclComm_t c : g->comms)
+            if (c && api) (void)api->destroy(c);
+    }
     for (GroupWorker* w : g->w) {
         {
             std::lock_guard<std::mutex> lk(w->m);
@@ -1026,6 +1163,41 @@ SM_API int sm_group_block_match_lr_u8(sm_group* g, const uint8_t* left, const ui
                                       uint8_t* right_disp_out, uint8_t* valid_mask_out, int out_pitch) {
     return group_bands(g, left, right, width, height, pitch, radius, num_disp, flags | SM_LR_CHECK, disp_out,
                        right_disp_out, valid_mask_out, out_pitch);
+}
+
+SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, const uint8_t* right, int width,
+                                          int height, int pitch, int radius, int num_disp, unsigned flags,
+                                          uint8_t* disp_out, int out_pitch) {
+    if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
+    if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (width <= 0 || height <= 0 || pitch < width || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d pitch %d out_pitch %d", width, height, pitch,
+                    out_pitch);
+    if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
+        return fail(SM_ERR_INVALID_ARG, "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED only; no LR, median, staged)",
+                    flags);
+    const bool guided = (flags & SM_AGG_GUIDED) != 0;
+    for (GroupWorker* w : g->w) {
+        int rc = check_geometry(w->h, width, height, width, radius, num_disp);
+        if (rc) return rc;
+        if (width > w->h->max_w || height > w->h->max_h || num_disp > w->h->max_d)
+            return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds member capacity", width, height, num_disp);
+    }
+    if (guided && radius > sm::kMaxFastRadius)
+        return fail(SM_ERR_INVALID_ARG, "guided aggregation: radius %d > %d", radius, sm::kMaxFastRadius);
+    int rc = group_comms(g);
+    if (rc) return rc;
+    const int n = (int)g->w.size();
+    std::vector<std::function<int()>> jobs;
+    for (int k = 0; k < n; ++k) {
+        sm_handle* h = g->w[k]->h;
+        ncclComm_t c = g->comms[k];
+        jobs.push_back([=]() -> int {
+            return dslice_member(h, c, k, n, left, right, width, height, pitch, radius, num_disp, guided, disp_out,
+                                 out_pitch);
+        });
+    }
+    return group_run(g, jobs);
 }
 
 SM_API int sm_group_block_match_batch_u8(sm_group* g, const uint8_t* const* lefts, const uint8_t* const* rights,

@@ -236,6 +236,20 @@ SM_API int sm_group_block_match_batch_u8(sm_group *g, const uint8_t *const *left
                                          const uint8_t *const *rights, int nframes, int width, int height,
                                          int pitch, int radius, int num_disp, unsigned flags,
                                          uint8_t *const *disps, int out_pitch);
+/* ONE frame sharded over the disparity range, the north star's split (Device.cu:43-61: every d
+ * plane is independent, so no halo): member k computes packed keys (SAD << 8 | d; guided:
+ * (int)(q * 2^14) << 8 | d) for d in [k*D/n, (k+1)*D/n) on its own device, one RCCL MIN
+ * reduce-scatter over xGMI gives each member the global argmin of 1/n of the pixels (the
+ * reference's first-smallest-d tie rule survives the MIN), each member finalises its pixels to
+ * uint8 (the Device.cu:37 threshold) and one RCCL all-gather assembles the map on every member;
+ * member 0's copy is downloaded into disp_out.  Bit-identical to sm_block_match_u8 for box
+ * aggregation; guided keys quantise q to 2^-14, so two fp32 costs closer than that may resolve
+ * differently from a single pass.  flags: 0 (box) or SM_AGG_GUIDED.  Members must be distinct
+ * devices; RCCL (librccl.so.1) is loaded on first use and one communicator per member is created
+ * with ncclCommInitAll. */
+SM_API int sm_group_dslice_block_match_u8(sm_group *g, const uint8_t *left, const uint8_t *right, int width,
+                                          int height, int pitch, int radius, int num_disp, unsigned flags,
+                                          uint8_t *disp_out, int out_pitch);
 
 #ifdef __cplusplus
 }

@@ -97,7 +97,9 @@ namespace detail {
 
 // SM_DEVICE=k picks the device; SM_DEVICES=a,b,... (two or more) also builds a group handle
 // (sm_create_group) over those devices, and blockMatching_gpu / testBM / getDisp then split each
-// frame into row bands, one per device (bit-identical results).
+// frame into row bands, one per device (bit-identical results).  SM_GROUP_MODE=dslice splits the
+// disparity range over the devices instead (sm_group_dslice_block_match_u8: RCCL MIN reduce-scatter
+// + all-gather over xGMI, the north star's split; bit-identical for box aggregation).
 struct Engine {
     sm_handle* h = nullptr;
     sm_group* g = nullptr;
@@ -133,7 +135,12 @@ struct Engine {
             h = nullptr;
             return false;
         }
-        if (devs.size() > 1 && sm_create_group((int)devs.size(), devs.data(), w, hgt, d, &g) != SM_OK) {
+        // the d-slice mode runs through a group even on one device (a one-rank communicator)
+        const char* mode = std::getenv("SM_GROUP_MODE");
+        std::vector<int> gdevs = devs;
+        if (gdevs.empty() && mode && std::string(mode) == "dslice") gdevs.push_back(dev);
+        if ((gdevs.size() > 1 || (mode && std::string(mode) == "dslice")) &&
+            sm_create_group((int)gdevs.size(), gdevs.data(), w, hgt, d, &g) != SM_OK) {
             std::cerr << "sm_create_group: " << sm_last_error_string() << std::endl;
             g = nullptr;
             return false;
@@ -165,7 +172,12 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     }
     detail::Engine& e = detail::engine();
     if (!e.ensure(cols, rows, searchRange)) return SM_ERR_DEVICE;
-    int rc = e.g ? sm_group_block_match_u8(e.g, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
+    const char* mode = std::getenv("SM_GROUP_MODE");
+    const bool dslice = e.g && mode && std::string(mode) == "dslice" && (flags & ~(unsigned)SM_AGG_GUIDED) == 0u;
+    int rc = dslice ? sm_group_dslice_block_match_u8(e.g, h_left.data, h_right.data, cols, rows,
+                                                     (int)detail::row_step(h_left), SADWindowSize, searchRange, flags,
+                                                     h_disparity.data, (int)detail::row_step(h_disparity))
+             : e.g ? sm_group_block_match_u8(e.g, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
                                            SADWindowSize, searchRange, flags, h_disparity.data,
                                            (int)detail::row_step(h_disparity))
                  : sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),

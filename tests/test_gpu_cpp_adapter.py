@@ -56,6 +56,21 @@ def test_single_frame_cpp_device_group(tmp_path, gray, bm_expected):
 
 
 @pytest.mark.gpu
+def test_single_frame_cpp_dslice_group(tmp_path, gray, bm_expected):
+    """SM_GROUP_MODE=dslice: the unchanged singleFrame() caller (Caller.cpp:19 -> blockMatching_gpu)
+    runs through the RCCL d-slice group mode (a one-rank communicator on the test box's one GPU:
+    slice keys, MIN reduce-scatter, finalise, all-gather) and still writes the golden map."""
+    _write_pgm(tmp_path / "l.pgm", gray["Books/view1"])
+    _write_pgm(tmp_path / "r.pgm", gray["Books/view5"])
+    env = dict(os.environ, SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
+               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD="4", SM_RANGE="64", SM_GROUP_MODE="dslice")
+    env.pop("SM_DEVICES", None)
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_read_pgm(tmp_path / "d.pgm"), bm_expected["Books/r4/D64"])
+
+
+@pytest.mark.gpu
 def test_remap_test_cpp(tmp_path, oracle):
     """remapTest() (Caller.cpp:27-74) end to end through stereo_bm.hpp: LoadDataBatch of the reference's
     calibration YAML -> Rectify (stereoRectify + GPU maps) -> remap_gpu on the Chess/Set2 pair at

@@ -72,3 +72,45 @@ def test_group_error_from_a_member():
         with pytest.raises(_capi.SMError) as e:
             g.match(L, R, 2, 16)
     assert e.value.code == _capi.SM_ERR_CAPACITY and "device 0" in str(e.value)
+
+
+# ---- RCCL d-slice mode (sm_group_dslice_block_match_u8): one member per distinct device --------
+@pytest.mark.parametrize("W,H,r,D", [(640, 333, 5, 128), (463, 370, 4, 64), (1920, 1080, 5, 256), (97, 31, 9, 37)])
+def test_group_dslice_one_member_box(single, W, H, r, D):
+    """On the one GPU of the test box the RCCL communicator has one rank: the slice is the whole
+    range, the reduce-scatter and all-gather are the identity, and the map must equal the single
+    handle bit for bit (odd pixel counts exercise the chunk padding)."""
+    import gpu_stereo_matching_amd as sm
+    L, R = _pair(W, H, D)
+    with sm.BlockMatcherGroup([0], 1920, 1080, 256) as g:
+        got = g.match_dslice(L, R, r, D)
+        got2 = g.match_dslice(L, R, r, D)          # the communicator is reused
+    want = single.match(L, R, r, D)
+    assert np.array_equal(got, want) and np.array_equal(got2, want)
+
+
+def test_group_dslice_one_member_guided(single):
+    import gpu_stereo_matching_amd as sm
+    W, H, r, D = 320, 240, 5, 64
+    L, R = _pair(W, H, D, seed=7)
+    with sm.BlockMatcherGroup([0], 1920, 1080, 256) as g:
+        g.set_guided_eps(EPS)
+        got = g.match_dslice(L, R, r, D, agg="guided")
+    want = single.match(L, R, r, D, agg="guided")
+    # the keys quantise q to 2^-14 (DESIGN §9): equal except where two fp32 costs are that close
+    assert (got == want).mean() >= 0.998
+
+
+def test_group_dslice_rejects_repeated_device_and_flags():
+    import gpu_stereo_matching_amd as sm
+    from gpu_stereo_matching_amd import _capi
+    L, R = _pair(64, 32, 16)
+    with sm.BlockMatcherGroup([0, 0], 256, 64, 64) as g:
+        with pytest.raises(_capi.SMError) as e:
+            g.match_dslice(L, R, 2, 16)
+        assert e.value.code == _capi.SM_ERR_INVALID_ARG and "distinct devices" in str(e.value)
+    out = np.empty((32, 64), np.uint8)
+    with sm.BlockMatcherGroup([0], 256, 64, 64) as g:
+        rc = g._lib.sm_group_dslice_block_match_u8(g._g, L.ctypes.data, R.ctypes.data, 64, 32, 64, 2, 16,
+                                                   _capi.SM_LR_CHECK, out.ctypes.data, 64)
+    assert rc == _capi.SM_ERR_INVALID_ARG
