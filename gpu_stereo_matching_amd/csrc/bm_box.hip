@@ -13,7 +13,7 @@
 //   valid      = d <= W - x   (the `col + d > cols` break, Device.cu:44)
 //   WTA        = first d with the smallest S_d below 50*win^2, else 0  (Device.cu:37-38,57,63)
 //
-// Tile geometry (R = radius, compile-time for R <= 7):
+// Tile geometry (R = radius, compile-time for R <= 15; the generic kernel beyond):
 //   64 CS columns (one per lane) -> TW = 64 - 2R output columns, TH = 32 output rows.
 //   Disparities are processed in pairs; wave w of NW owns the contiguous pair range
 //   [w*npairs/NW, (w+1)*npairs/NW) end to end (phase V -> its private CS plane -> phase H), so
@@ -39,8 +39,13 @@ constexpr int kWaves = kWideRight<RIGHT, R> ? 8 : 4;
 // the extra live values push the fused loop past 128 VGPRs (r = 3: NQ = 16)
 template <int R>
 constexpr bool kPairedScatter = (R != 3);
+// radius 8..15 (WIDE): the packed u16 column sums still fit (<= (32 + 2r) * 255), the window sums do
+// not, so phase H keeps the two halves in separate u32 sums; the longer CS rows and the 2r+1-row
+// ring need more than 128 VGPRs (2 waves/SIMD)
+template <int R>
+constexpr bool kWideR = R > 7;
 template <bool RIGHT, int R>
-constexpr int kMinWavesPerEU = (RIGHT && !kWideRight<RIGHT, R>) ? 2 : 4;
+constexpr int kMinWavesPerEU = ((RIGHT && !kWideRight<RIGHT, R>) || kWideR<R>) ? 2 : 4;
 constexpr int kTileH = 32;        // output rows per tile (48: 4 % slower, 3 waves/SIMD)
 constexpr int kNB = kTileH / 16;   // 16-row CS hand-off blocks per tile
 constexpr int kPairs = 4;
@@ -282,9 +287,42 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                     v[2 * q + 0] = x2.x;
                     v[2 * q + 1] = x2.y;
                 }
-                uint32_t S = 0u;
+                // WIDE: the two u16 halves of each CS word summed separately (window sums need 18 bits)
+                uint32_t S = 0u, Sh = 0u;
 #pragma unroll
-                for (int k = 0; k < 2 * R; ++k) S += v[k];
+                for (int k = 0; k < 2 * R; ++k) {
+                    if constexpr (kWideR<R>) {
+                        S += v[k] & 0xFFFFu;
+                        Sh += v[k] >> 16;
+                    } else {
+                        S += v[k];
+                    }
+                }
+                // keys (S << 8 | d): packed halves by v_perm; WIDE halves by v_lshl_or
+                auto add_in = [&](uint32_t x) {
+                    if constexpr (kWideR<R>) {
+                        S += x & 0xFFFFu;
+                        Sh += x >> 16;
+                    } else {
+                        S += x;
+                    }
+                };
+                auto sub_out = [&](uint32_t x) {
+                    if constexpr (kWideR<R>) {
+                        S -= x & 0xFFFFu;
+                        Sh -= x >> 16;
+                    } else {
+                        S -= x;
+                    }
+                };
+                auto key_lo = [&]() -> uint32_t {
+                    if constexpr (kWideR<R>) return (S << 8) | (dsel & 0xFFu);
+                    else return __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
+                };
+                auto key_hi = [&]() -> uint32_t {
+                    if constexpr (kWideR<R>) return (Sh << 8) | (dsel >> 8);
+                    else return __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                };
                 // RIGHT: klo of output o goes to u_o = x_o - d, khi to u_o - 1 = u_{o-1}; the two
                 // candidates of one u are min'ed in registers, one ds_min_u32 per u
                 uint32_t* rrow = rb + (h * G::HALF + hj) * G::RBW + (obase - d + DMAX + 1);   // + o: u_o
@@ -292,9 +330,9 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                 if (!dm) {
 #pragma unroll
                     for (int o = 0; o < G::NQ; ++o) {
-                        S += v[o + 2 * R];
-                        const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
-                        const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                        add_in(v[o + 2 * R]);
+                        const uint32_t klo = key_lo();
+                        const uint32_t khi = key_hi();
                         best[h][o] = min(best[h][o], min(klo, khi));
                         if constexpr (RIGHT) {
                             // outputs past TW (last quarter only) read CS columns outside the tile
@@ -308,16 +346,16 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                                 atomicMin(rrow + o, klo);
                             }
                         }
-                        S -= v[o];
+                        sub_out(v[o]);
                     }
                 } else {
 #pragma unroll
                     for (int o = 0; o < G::NQ; ++o) {
-                        S += v[o + 2 * R];
+                        add_in(v[o + 2 * R]);
                         const int x = x0 + obase + o;
                         const int lim = a.valid_mode == 0 ? (W - x) : x;
-                        const uint32_t klo = __builtin_amdgcn_perm(S, dsel, 0x0C050400u);
-                        const uint32_t khi = __builtin_amdgcn_perm(S, dsel, 0x0C070601u);
+                        const uint32_t klo = key_lo();
+                        const uint32_t khi = key_hi();
                         const uint32_t mlo = (d <= lim && d < d_hi) ? klo : 0xFFFFFFFFu;
                         const uint32_t mhi = (d + 1 <= lim && d + 1 < d_hi) ? khi : 0xFFFFFFFFu;
                         best[h][o] = min(best[h][o], min(mlo, mhi));
@@ -333,7 +371,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                                 atomicMin(rrow + o, rlo);
                             }
                         }
-                        S -= v[o];
+                        sub_out(v[o]);
                     }
                 }
                 if constexpr (RIGHT && kPairedScatter<R>) atomicMin(rrow + G::NQ - 1, plo);
@@ -485,7 +523,7 @@ size_t partial_bytes_r(int W, int H, int D, int batch) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Generic path for radius > 7 (u16 packing would overflow): direct window sum per (pixel, d)
+// Generic path for radius > 15 (the u16 column prefix would overflow): direct window sum per (pixel, d)
 // straight from the reference formulation.  Correct for any radius; not a performance path.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void box_match_generic_kernel(MatchArgs a, int64_t total) {
@@ -535,6 +573,14 @@ hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s) {
         case 5: return launch_r<5, false>(a, batch, nullptr, s);
         case 6: return launch_r<6, false>(a, batch, nullptr, s);
         case 7: return launch_r<7, false>(a, batch, nullptr, s);
+        case 8: return launch_r<8, false>(a, batch, nullptr, s);
+        case 9: return launch_r<9, false>(a, batch, nullptr, s);
+        case 10: return launch_r<10, false>(a, batch, nullptr, s);
+        case 11: return launch_r<11, false>(a, batch, nullptr, s);
+        case 12: return launch_r<12, false>(a, batch, nullptr, s);
+        case 13: return launch_r<13, false>(a, batch, nullptr, s);
+        case 14: return launch_r<14, false>(a, batch, nullptr, s);
+        case 15: return launch_r<15, false>(a, batch, nullptr, s);
         default: return launch_box_match_generic(a, batch, s);
     }
 }
@@ -549,6 +595,14 @@ size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch) {
         case 5: return partial_bytes_r<5>(W, H, D, batch);
         case 6: return partial_bytes_r<6>(W, H, D, batch);
         case 7: return partial_bytes_r<7>(W, H, D, batch);
+        case 8: return partial_bytes_r<8>(W, H, D, batch);
+        case 9: return partial_bytes_r<9>(W, H, D, batch);
+        case 10: return partial_bytes_r<10>(W, H, D, batch);
+        case 11: return partial_bytes_r<11>(W, H, D, batch);
+        case 12: return partial_bytes_r<12>(W, H, D, batch);
+        case 13: return partial_bytes_r<13>(W, H, D, batch);
+        case 14: return partial_bytes_r<14>(W, H, D, batch);
+        case 15: return partial_bytes_r<15>(W, H, D, batch);
         default: return 0;
     }
 }
@@ -566,6 +620,14 @@ hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t
         case 5: return launch_r<5, true>(a, batch, &ro, s);
         case 6: return launch_r<6, true>(a, batch, &ro, s);
         case 7: return launch_r<7, true>(a, batch, &ro, s);
+        case 8: return launch_r<8, true>(a, batch, &ro, s);
+        case 9: return launch_r<9, true>(a, batch, &ro, s);
+        case 10: return launch_r<10, true>(a, batch, &ro, s);
+        case 11: return launch_r<11, true>(a, batch, &ro, s);
+        case 12: return launch_r<12, true>(a, batch, &ro, s);
+        case 13: return launch_r<13, true>(a, batch, &ro, s);
+        case 14: return launch_r<14, true>(a, batch, &ro, s);
+        case 15: return launch_r<15, true>(a, batch, &ro, s);
         default: return hipErrorInvalidValue;
     }
 }

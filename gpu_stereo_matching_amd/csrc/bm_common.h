@@ -35,11 +35,14 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
     return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
 }
 constexpr int kMaxFastRadius = 7;  // u16 packed sums stay < 2^16 up to r = 7 (15*15*255 = 57375)
+// fused box matcher (bm_box.hip): u16 packed column prefixes stay < 2^16 up to r = 15
+// ((32 + 30) * 255 = 15810); r 8..15 sum the window's two halves in u32
+constexpr int kMaxBoxRadius = 15;
 
 // Host-side launchers (bm_box.hip, bm_aux.hip).
 hipError_t launch_box_match(const MatchArgs& a, int batch, hipStream_t s);
 hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s);
-// Box matching + right view (+ LR check) in two launches (radius <= kMaxFastRadius, d_lo == 0).
+// Box matching + right view (+ LR check) in two launches (radius <= kMaxBoxRadius, d_lo == 0).
 // check = 1: a.disp receives the checked left disparity, right_out/mask_out (optional) dR and the
 // valid mask.  check = 0: a.disp the unchecked left map and right_out (required) dR.
 hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,

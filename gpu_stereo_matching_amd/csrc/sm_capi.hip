@@ -211,7 +211,7 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     constexpr int kMedianRadius = 3;   // MeanFilter(disp, disp, 3)
     const int64_t P = (int64_t)W * H;
     const int64_t PB = P * batch;
-    const bool fused_right = lr && !guided && radius <= sm::kMaxFastRadius;
+    const bool fused_right = lr && !guided && radius <= sm::kMaxBoxRadius;
     const bool guided_right = lr && guided;   // right view fused into the guided pass (bm_guided.hip)
     if ((flags & SM_STAGED) != 0) {
         if (guided || lr || radius > sm::kMaxFastRadius)

@@ -58,8 +58,9 @@ def test_synthetic_edge_cases(matcher, synth_expected):
         assert np.array_equal(got, synth_expected[f"{n}/disp"]), n
 
 
-@pytest.mark.parametrize("r", list(range(0, 10)))
+@pytest.mark.parametrize("r", list(range(0, 17)))
 def test_every_radius(matcher, oracle, r):
+    """r 0..7: packed u16 window sums; 8..15: the same kernel with u32 window halves; 16: generic."""
     rng = np.random.default_rng(100 + r)
     H, W, D = 45, 150, 40
     L = rng.integers(0, 256, (H, W), dtype=np.uint8)
@@ -180,14 +181,44 @@ def test_lr_golden(matcher, gray, bm_expected):
 
 
 @pytest.mark.parametrize("r,D", [(0, 8), (1, 16), (2, 1), (3, 37), (4, 64), (5, 128), (6, 256), (7, 100), (8, 48),
-                                 (5, 2), (5, 129)])
+                                 (5, 2), (5, 129), (11, 64), (15, 256), (16, 40)])
 def test_lr_random(matcher, oracle, r, D):
-    """r <= 7: right view fused into the matching pass (rpart + reduce); r = 8: mirrored second pass."""
+    """r <= 15: right view fused into the matching pass (rpart + reduce); r = 16: mirrored second pass."""
     L, R = oracle.synth_pair(r * 7 + D, 257, 61, max(D, 16))
     disp, rd, chk, mask = oracle.box_lr(L, R, r, D)
     c, rr, mm = matcher.match_lr(L, R, r, D)
     assert np.array_equal(rr, rd), (r, D)
     assert np.array_equal(c, chk) and np.array_equal(mm, mask), (r, D)
+
+
+@pytest.mark.parametrize("r", [8, 11, 15])
+@pytest.mark.parametrize("D", [64, 256])
+def test_wide_radius_fast_path(matcher, oracle, torch, r, D):
+    """Radius 8..15 (the reference's SADWindowSize is unbounded, Device.cu:46-56) on the fused kernel:
+    window sums up to 31^2 * 255 need the u32 halves; bit-exact with the separable oracle, host and
+    batched device path, plain and with the LR check."""
+    L, R = oracle.synth_pair(1000 + 10 * r + D, 333, 150, D)
+    want = oracle.box_disp(L, R, r, D)
+    assert np.array_equal(matcher.match(L, R, r, D), want), (r, D)
+    L2, R2 = oracle.synth_pair(2000 + r, 333, 150, D)
+    Lt = torch.from_numpy(np.stack([L, L2])).cuda()
+    Rt = torch.from_numpy(np.stack([R, R2])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[0].cpu().numpy(), want) and np.array_equal(out[1].cpu().numpy(),
+                                                                          oracle.box_disp(L2, R2, r, D))
+    _, rd, chk, mask = oracle.box_lr(L, R, r, D)
+    c, rr, mm = matcher.match_lr(L, R, r, D)
+    assert np.array_equal(rr, rd) and np.array_equal(c, chk) and np.array_equal(mm, mask), (r, D)
+
+
+def test_wide_radius_saturated(matcher, oracle):
+    """r = 15 on 0/255 images: window sums reach 961 * 255, the largest the u32 halves carry."""
+    rng = np.random.default_rng(15)
+    L = (rng.integers(0, 2, (96, 200)) * 255).astype(np.uint8)
+    R = 255 - L
+    for D in (16, 100):
+        assert np.array_equal(matcher.match(L, R, 15, D), oracle.box_disp(L, R, 15, D))
 
 
 @pytest.mark.parametrize("W,H,r,D", [(40, 30, 3, 64), (53, 7, 5, 64), (3, 5, 1, 8), (1000, 33, 5, 256), (600, 97, 7, 192)])

@@ -44,10 +44,10 @@ def test_median_flag_box(matcher, oracle, gray):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("r,D", [(5, 64), (3, 48), (8, 32)])
+@pytest.mark.parametrize("r,D", [(5, 64), (3, 48), (8, 32), (16, 24)])
 def test_median_then_lr(matcher, oracle, r, D):
     """Both WTA maps median-filtered before the LR check (StereoDisparity.cpp:119-147);
-    r = 8 exercises the mirrored right view."""
+    r = 8 runs the fused right view's u32 window halves, r = 16 the mirrored right view."""
     L, R = oracle.synth_pair(r + D, 301, 97, max(D, 16))
     disp, cost = oracle.box_disp(L, R, r, D, want_cost=True)
     left_m = oracle.median(disp, 3)
