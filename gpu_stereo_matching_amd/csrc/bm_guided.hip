@@ -42,6 +42,10 @@
 #include "bm_common.h"
 #include "bm_guided.h"
 
+// The addtid stores set M0 inside their own asm statement and name it clobbered; these kernels have
+// no other M0 user (checked in the ISA), so clang's reserved-register warning is noise here.
+#pragma clang diagnostic ignored "-Winline-asm"
+
 namespace sm {
 namespace {
 
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // S1V state: this wave walks P rows [a0, a0 + NV) (rows past PH are pad rows that only reach
     // the pad rows of cs); lane = P column c
     const int a0 = wave * G::RPW;
+    const uint32_t m0_cs = (uint32_t)(a0 * G::CSS * 4);   // cs is the first LDS block
     const int c = lane;
     const int xc = px0 + c;
     const bool col_in = xc >= 0 && xc < W;
@@ -265,7 +270,15 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             T = __umul24(ad, mul[k]) + T;
             if (k >= 2 * R) {
                 const uint32_t old = (k == 2 * R) ? 0u : Tp[(k - 2 * R - 1) % (2 * R + 1)];
-                cs[(a0 + k - 2 * R) * G::CSS + c] = m ? T - old : 0u;
+                const uint32_t val = m ? T - old : 0u;
+                // cs[(a0 + k - 2R) * CSS + lane]: lane-consecutive dwords, so ds_write_addtid_b32
+                // (M0 = this wave's first cs row; 2 LDS cycles per store instead of 4).  An SALU write
+                // of M0 needs one wait state before an add-TID LDS instruction reads it (the compiler
+                // does not see the hazard inside the asm): s_nop 0.
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:%2"
+                             :
+                             : "s"(m0_cs), "v"(val), "i"((k - 2 * R) * G::CSS * 4)
+                             : "memory", "m0");
             }
             Tp[k % (2 * R + 1)] = T;
         }
@@ -327,7 +340,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             asm("v_mul_i32_i24 %0, %1, %2" : "=v"(num) : "v"(nSI[o]), "v"(sp));
             asm("v_mad_i32_i24 %0, %1, %2, %0" : "+v"(num) : "v"(nN[o]), "v"(sip));
             const float a = (float)num * invden[o];
-            const float b = __builtin_fmaf(-a, fSI[o], (float)sp) * invN[o];
+            // float(Sp) without v_cvt (a quarter-rate op here): Sp < 2^22, float(2^23 + Sp) is exact
+            const float fsp = __builtin_bit_cast(float, 0x4B000000u | sp) - 8388608.0f;
+            const float b = __builtin_fmaf(-a, fSI[o], fsp) * invN[o];
             // one ds_write_b64 (the compiler emits ds_write2_b32 for a float2 store here)
             asm volatile("ds_write_b64 %0, %1 offset:%2"
                          :

@@ -1,0 +1,40 @@
+"""Bit-compare guided (and box) maps of libsm_hip.so builds: python tools/variant_diff.py base.so other.so ...
+Each library runs in its own process (one HIP library per process); outputs are compared with the first."""
+import os, subprocess, sys, tempfile
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_one(lib, out):
+    code = f"""
+import sys; sys.path.insert(0, {ROOT!r})
+import numpy as np, gpu_stereo_matching_amd._capi as C
+C.load({lib!r})
+import gpu_stereo_matching_amd as sm
+g = np.load({os.path.join(ROOT, 'tests', 'golden', 'middlebury_gray.npz')!r})
+res = {{}}
+L, R = g['Art_/view1'], g['Art_/view5']
+sL, sR = sm.synth_pair(7, 1920, 1080, 128)
+with sm.BlockMatcher(0, 1920, 1080, 256) as m:
+    for r in (1, 3, 5):
+        res[f'art_g{{r}}'] = m.match(L, R, r, 64, agg='guided')
+        chk, rd, mask = m.match_lr(L, R, r, 64, agg='guided')
+        res[f'art_glr{{r}}'] = np.stack([chk, rd, mask])
+    res['syn_g5'] = m.match(sL, sR, 5, 128, agg='guided')
+np.savez({out!r}, **res)
+"""
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300)
+
+
+libs = sys.argv[1:]
+tmp = tempfile.mkdtemp()
+outs = []
+for i, lib in enumerate(libs):
+    o = os.path.join(tmp, f"{i}.npz")
+    run_one(os.path.abspath(lib), o)
+    outs.append(np.load(o))
+for lib, o in zip(libs[1:], outs[1:]):
+    for k in outs[0].files:
+        a, b = outs[0][k], o[k]
+        print(f"{os.path.basename(lib):14s} {k:10s} differing pixels: {int((a != b).sum())} of {a.size}")
