@@ -134,17 +134,33 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
 // K3: 8 pixels per thread, one 16-B nontemporal load per d plane (the volume is streamed once and
 // is larger than the MALL).  The loads of kWtaUnroll consecutive planes are issued before any of
 // them is used, so each wave keeps kWtaUnroll KB in flight (one plane at a time measured 4.4 TB/s:
-// a read stream needs ~20 KB in flight per CU at HBM latency).
-constexpr int kWtaUnroll = 8;
+// a read stream needs ~20 KB in flight per CU at HBM latency).  The d range is split over SPLIT
+// thread groups of one workgroup (same pixels, consecutive d ranges), merged through LDS in d order:
+// SPLIT times the workgroups of a one-group-per-pixel-block grid, for the same bytes per thread.
+#ifndef SM_WTA_UNROLL
+#define SM_WTA_UNROLL 8
+#endif
+#ifndef SM_WTA_SPLIT
+#define SM_WTA_SPLIT 4   // 1080p D=128 same-box A/B: 102.6 us (1 group), 99.2 (4 groups)
+#endif
+constexpr int kWtaUnroll = SM_WTA_UNROLL;
+// nontemporal: plain loads measured 135 us against 103 (one group)
+__device__ __forceinline__ u32x4 ld_plane(const u32x4* p) { return __builtin_nontemporal_load(p); }
+constexpr int kWtaSplit = SM_WTA_SPLIT;
 
 __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restrict__ sad, int W, int H, int D,
                                                          uint32_t seed_key, uint8_t* __restrict__ disp,
                                                          int out_pitch) {
     constexpr int NPX = 8;
+    constexpr int TPG = kST / kWtaSplit;             // threads per d group
+    __shared__ uint32_t part[kWtaSplit > 1 ? kWtaSplit - 1 : 1][TPG][NPX + 1];
     const int64_t P = (int64_t)W * H;
-    const int64_t p0 = ((int64_t)blockIdx.x * kST + threadIdx.x) * NPX;
-    if (p0 >= P) return;
-    const int n = P - p0 < NPX ? (int)(P - p0) : NPX;
+    const int grp = threadIdx.x / TPG, gt = threadIdx.x - grp * TPG;
+    const int64_t p0 = ((int64_t)blockIdx.x * TPG + gt) * NPX;
+    const int n = p0 >= P ? 0 : (P - p0 < NPX ? (int)(P - p0) : NPX);
+    // this group's planes: [d_lo, d_hi), whole unroll blocks except the last group
+    const int dper = ((D + kWtaSplit - 1) / kWtaSplit + kWtaUnroll - 1) / kWtaUnroll * kWtaUnroll;
+    const int d_lo = min(D, grp * dper), d_hi = min(D, d_lo + dper);
     int lim[NPX];
     uint32_t best[NPX];
 #pragma unroll
@@ -160,11 +176,11 @@ __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restr
     if (vec) {
         const u32x4* base = reinterpret_cast<const u32x4*>(sad + p0);
         const int64_t pstride = P / 8;                // one plane in u32x4 units
-        int d = 0;
-        for (; d + kWtaUnroll <= D; d += kWtaUnroll) {
+        int d = d_lo;
+        for (; d + kWtaUnroll <= d_hi; d += kWtaUnroll) {
             u32x4 v[kWtaUnroll];
 #pragma unroll
-            for (int u = 0; u < kWtaUnroll; ++u) v[u] = __builtin_nontemporal_load(base + (int64_t)(d + u) * pstride);
+            for (int u = 0; u < kWtaUnroll; ++u) v[u] = ld_plane(base + (int64_t)(d + u) * pstride);
 #pragma unroll
             for (int u = 0; u < kWtaUnroll; ++u)
 #pragma unroll
@@ -173,21 +189,33 @@ __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restr
                     take(v[u][q] >> 16, 2 * q + 1, d + u);
                 }
         }
-        for (; d < D; ++d) {
-            const u32x4 v = __builtin_nontemporal_load(base + (int64_t)d * pstride);
+        for (; d < d_hi; ++d) {
+            const u32x4 v = ld_plane(base + (int64_t)d * pstride);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 take(v[q] & 0xFFFFu, 2 * q, d);
                 take(v[q] >> 16, 2 * q + 1, d);
             }
         }
-    } else {
-        for (int d = 0; d < D; ++d) {
+    } else if (n > 0) {
+        for (int d = d_lo; d < d_hi; ++d) {
             const uint16_t* pl = sad + (int64_t)d * P + p0;
 #pragma unroll
             for (int k = 0; k < NPX; ++k)
                 if (k < n) take(pl[k], k, d);
         }
+    }
+    if constexpr (kWtaSplit > 1) {
+        // keys (SAD << 8 | d) order by cost, then d: a plain min over the groups is the first-d argmin
+        if (grp > 0)
+#pragma unroll
+            for (int k = 0; k < NPX; ++k) part[grp - 1][gt][k] = best[k];
+        __syncthreads();
+        if (grp > 0) return;
+#pragma unroll
+        for (int g = 0; g < kWtaSplit - 1; ++g)
+#pragma unroll
+            for (int k = 0; k < NPX; ++k) best[k] = min(best[k], part[g][gt][k]);
     }
 #pragma unroll
     for (int k = 0; k < NPX; ++k) {
@@ -235,7 +263,7 @@ hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, in
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, uint32_t seed_key, uint8_t* disp,
                              int out_pitch, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
-    const int64_t blocks = (P + 8 * kST - 1) / (8 * kST);
+    const int64_t blocks = (P + 8 * (kST / kWtaSplit) - 1) / (8 * (kST / kWtaSplit));
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     hipLaunchKernelGGL(volume_wta_kernel, dim3((unsigned)blocks), dim3(kST), 0, s, sad, W, H, D, seed_key, disp,
                        out_pitch);

@@ -103,6 +103,18 @@ int main() {
     (void)hipMalloc(&o, 64);
     (void)hipMemset(a, 1, bytes);
     (void)hipMemset(b, 2, bytes);
+    if (getenv("HBM_VENDOR")) {
+        // the runtime's own fill and device-to-device copy kernels as reference ceilings
+        timeit("hipMemsetAsync 1 GiB (write)", bytes, [&] { (void)hipMemsetAsync(b, 3, bytes, 0); });
+        timeit("hipMemsetD32Async 1 GiB (write)", bytes,
+               [&] { (void)hipMemsetD32Async((hipDeviceptr_t)b, 0x01020304u, bytes / 4, 0); });
+        timeit("hipMemcpyAsync D2D 1 GiB (r+w bytes)", 2.0 * bytes,
+               [&] { (void)hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0); });
+        timeit("write 16B nt, 16384 blocks", bytes, [&] { wr<true><<<16384, 256>>>(b, n); });
+        timeit("write 16B nt, 65536 blocks", bytes, [&] { wr<true><<<65536, 256>>>(b, n); });
+        timeit("write 16B chunk 4/lane nt", bytes, [&] { wrc<4, true><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        return 0;
+    }
     if (getenv("HBM_WRITE_ONLY")) {
         for (int blocks : {2048, 8192, 32768}) {
             char nm[64];
