@@ -477,6 +477,40 @@ def test_frame_stream_camera_chain(matcher, oracle, mode):
             assert np.array_equal(got[i], want[i])
 
 
+def test_capture_loop_replay(matcher, oracle, tmp_path):
+    """capture.run_loop over photo()-style saved pairs (Left_<n>/Right_<n>, Utility.cpp:217-218): PNG
+    BGR frames -> GPU gray -> the calibration's rectification -> match, 2 pairs per launch over 5 pairs
+    (a padded last batch); each map, delivered in pair order and written as disp_<n>.png, equals the
+    oracle chain bit for bit."""
+    import os
+    from PIL import Image
+    from gpu_stereo_matching_amd import calib
+    from gpu_stereo_matching_amd.capture import PairSequence, run_loop
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    W, H, r, D = 320, 200, 4, 48
+    rng = np.random.default_rng(11)
+    want = {}
+    K1, K2, d1, d2, Rm, T = calib.load_data_batch(os.path.join(golden, "Calib_Data_OpenCV.yml"))
+    R1, R2, P1, P2, _ = calib.stereo_rectify(K1, d1, K2, d2, (W, H), Rm, T)
+    maps = (*oracle.init_rectify_map(K1, d1, R1, P1, W, H), *oracle.init_rectify_map(K2, d2, R2, P2, W, H))
+    for n in (1, 3, 4, 8, 12):
+        Lb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        Rb = np.roll(Lb, -5 - n, axis=1)
+        Image.fromarray(Lb[:, :, ::-1]).save(tmp_path / f"Left_{n}.png")    # stored as RGB, read back as BGR
+        Image.fromarray(Rb[:, :, ::-1]).save(tmp_path / f"Right_{n}.png")
+        gl = oracle.remap(oracle.bgr_to_gray(Lb), maps[0], maps[1])
+        gr = oracle.remap(oracle.bgr_to_gray(Rb), maps[2], maps[3])
+        want[n] = oracle.box_disp(gl, gr, r, D)
+    got = {}
+    out = tmp_path / "maps"
+    order = run_loop(PairSequence(str(tmp_path)), matcher, r, D, rectify_maps=maps, batch=2,
+                     on_map=lambda n, d: got.__setitem__(n, d.copy()), out_dir=str(out))
+    assert order == [1, 3, 4, 8, 12]
+    for n, w in want.items():
+        assert np.array_equal(got[n], w), n
+        assert np.array_equal(np.asarray(Image.open(out / f"disp_{n}.png")), w), n
+
+
 @pytest.mark.parametrize("W,H,D", [(64, 16, 8), (333, 77, 100), (1920, 1080, 128), (5, 3, 7)])
 def test_ad_volume(matcher, oracle, torch, W, H, D):
     """PreCal / kernalPreCal_V2 (row a1) as a standalone HBM-bound kernel, bit-exact."""

@@ -64,3 +64,27 @@ def test_device_pair_checks_reject_bad_inputs():
         sm._check_device_pair(a[None], a[None])
     with pytest.raises(ValueError, match="device"):
         sm._check_device_pair(a, a)
+
+
+def test_pair_sequence_order_and_bgr(tmp_path):
+    """capture.PairSequence: photo()'s Left_<n>/Right_<n> files (Utility.cpp:217-218) in numeric order
+    (10 after 2), unmatched left files skipped, frames returned as BGR like cv::imread."""
+    from PIL import Image
+    from gpu_stereo_matching_amd.capture import PairSequence
+    rng = np.random.default_rng(3)
+    frames = {}
+    for n in (0, 2, 10):
+        lr = [rng.integers(0, 256, (6, 9, 3), dtype=np.uint8) for _ in range(2)]
+        frames[n] = lr
+        Image.fromarray(lr[0]).save(tmp_path / f"Left_{n}.png")    # written as RGB
+        Image.fromarray(lr[1]).save(tmp_path / f"Right_{n}.png")
+    Image.fromarray(frames[0][0]).save(tmp_path / "Left_7.png")      # no Right_7
+    seq = PairSequence(str(tmp_path))
+    assert len(seq) == 3
+    got = list(seq)
+    assert [g[0] for g in got] == [0, 2, 10]
+    for n, left, right in got:
+        assert np.array_equal(left, frames[n][0][:, :, ::-1])
+        assert np.array_equal(right, frames[n][1][:, :, ::-1])
+    small = list(PairSequence(str(tmp_path), size=(3, 2)))
+    assert small[0][1].shape == (2, 3, 3)
