@@ -153,6 +153,27 @@ class BlockMatcher:
                                                     num_disp, _flags(agg, lr_check), out.ctypes.data, W))
         return out
 
+    def segment_tree(self, left_bgr, right_bgr, max_level: int = 60, scale: int = 4, sigma: float = 0.1) -> np.ndarray:
+        """STMatching's segment-tree stereo, ST-1 (stereo_disparity_normal, StereoDisparity.cpp:57-89):
+        HxWx3 uint8 BGR frames -> colour + gradient cost over d < max_level -> tree aggregation on the
+        left view's colour tree -> WTA -> 7x7 median -> x scale.  Cost, filter, WTA and median on the GPU,
+        the tree on the host (as the reference).  Defaults as STMatching/main.cpp:49-51."""
+        Lb = np.ascontiguousarray(left_bgr, dtype=np.uint8)
+        Rb = np.ascontiguousarray(right_bgr, dtype=np.uint8)
+        if Lb.ndim != 3 or Lb.shape[2] != 3 or Lb.shape != Rb.shape:
+            raise ValueError("expected two equal HxWx3 uint8 BGR frames")
+        H, W, _ = Lb.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_segment_tree_match_bgr_u8(self._h, Lb.ctypes.data, Rb.ctypes.data, W, H, 3 * W,
+                                                           max_level, scale, sigma, out.ctypes.data, W))
+        return out
+
+    def segment_tree_stats(self) -> Tuple[float, float, int]:
+        """(host tree-build ms, whole-call ms, BFS levels of the tree) of the last segment_tree call."""
+        t, a, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        _capi.check(self._lib.sm_last_segment_tree_stats(self._h, ctypes.byref(t), ctypes.byref(a), ctypes.byref(n)))
+        return t.value, a.value, n.value
+
     def cvt_color(self, bgr) -> np.ndarray:
         """cvtColor_gpu (Device.cuh:52) on host memory: HxWx3|4 uint8 BGR(A) -> gray, OpenCV 2.4 weights."""
         B = np.ascontiguousarray(bgr, dtype=np.uint8)

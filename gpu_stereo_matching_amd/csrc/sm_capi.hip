@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <functional>
@@ -24,6 +25,7 @@
 #include "../../include/sm_hip.h"
 #include "bm_common.h"
 #include "bm_guided.h"
+#include "bm_segtree.h"
 
 struct sm_handle {
     int device = 0;
@@ -64,6 +66,11 @@ struct sm_handle {
     // key chunk, its uint8 chunk and the gathered map (grown on demand)
     uint8_t* d_dsl = nullptr;
     size_t dsl_bytes = 0;
+    // segment-tree path (sm_segment_tree_match_bgr_u8): device workspace and the last call's stats
+    sm::StWorkspace st;
+    sm::StStats st_stats;
+    float st_total_ms = 0.f;
+    bool st_valid = false;
     // staged box path: events around the last frame's AD / SAD / WTA kernels (sm_last_staged_kernel_ms)
     hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool kev_valid = false;
@@ -1026,6 +1033,55 @@ SM_API int sm_median_u8_device(sm_handle* h, const uint8_t* d_src, int width, in
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(sm::launch_median(d_src, width, height, pitch, (int64_t)pitch * height, 1, radius, d_dst, dst_pitch,
                              (int64_t)dst_pitch * height, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_segment_tree_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
+                                        int height, int pitch, int max_level, int scale, float sigma,
+                                        uint8_t* disp_out, int out_pitch) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!left_bgr || !right_bgr || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (width < 2 || height < 1 || pitch < 3 * width || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d (pitch %d, out_pitch %d)", width, height, pitch,
+                    out_pitch);
+    if (max_level < 1 || max_level > sm::kMaxDisp) return fail(SM_ERR_INVALID_ARG, "max_level %d out of [1,256]", max_level);
+    if (scale < 0) return fail(SM_ERR_INVALID_ARG, "scale %d < 0", scale);
+    if (!(sigma > 0.f)) return fail(SM_ERR_INVALID_ARG, "sigma must be > 0");
+    if (width > h->max_w || height > h->max_h || max_level > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity %dx%d/D=%d", width, height, max_level,
+                    h->max_w, h->max_h, h->max_d);
+    SM_HIP(hipSetDevice(h->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t row = (size_t)width * 3, need = 2 * row * height;
+    if (h->bgr_bytes < need) {
+        if (h->d_bgr) (void)hipFree(h->d_bgr);
+        h->d_bgr = nullptr;
+        h->bgr_bytes = 0;
+        SM_HIP(hipMalloc(&h->d_bgr, need));
+        h->bgr_bytes = need;
+    }
+    hipStream_t s = h->stream;
+    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    uint8_t* dl = h->d_bgr;
+    uint8_t* dr = h->d_bgr + row * height;
+    SM_HIP(copy2d(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
+    h->st_valid = false;
+    SM_HIP(sm::segment_tree_match(h->st, dl, dr, width, height, (int)row, max_level, scale, sigma, 1200.0f, h->d_disp, s,
+                                  &h->st_stats));
+    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    h->st_total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    h->st_valid = true;
+    return SM_OK;
+}
+
+SM_API int sm_last_segment_tree_stats(sm_handle* h, float* tree_ms, float* total_ms, int* levels) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!h->st_valid) return fail(SM_ERR_INVALID_ARG, "no segment-tree call has completed on this handle");
+    if (tree_ms) *tree_ms = h->st_stats.tree_ms;
+    if (total_ms) *total_ms = h->st_total_ms;
+    if (levels) *levels = h->st_stats.levels;
     return SM_OK;
 }
 

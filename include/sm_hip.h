@@ -210,6 +210,19 @@ SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const ui
                                  int width, int height, int pitch, int channels, int radius,
                                  int num_disp, unsigned flags, uint8_t *disp_out, int out_pitch);
 
+/* STMatching's segment-tree stereo, ST-1 (stereo_disparity_normal, StereoDisparity.cpp:57-89; SURVEY
+ * §8f rank 4): BGR host frames (3 bytes per pixel, row pitch `pitch`) -> truncated colour + gradient
+ * cost over d in [0, max_level) -> segment-tree aggregation on the left view's colour tree
+ * (sigma, TAU = 1200) -> WTA -> 7x7 median -> disparity x scale (saturated), uint8 [height][out_pitch].
+ * The cost, the filter, the WTA and the median run on the GPU; the tree (a sequential Kruskal / BFS,
+ * as in the reference) is built on the host from the GPU's edge weights.  Synchronous.
+ * Reference defaults (STMatching/main.cpp:49-51): max_level 60, scale 4, sigma 0.1. */
+SM_API int sm_segment_tree_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,
+                                        int width, int height, int pitch, int max_level, int scale, float sigma,
+                                        uint8_t *disp_out, int out_pitch);
+/* last segment-tree call: host tree-build time, whole-call time (ms) and the tree's BFS level count */
+SM_API int sm_last_segment_tree_stats(sm_handle *h, float *tree_ms, float *total_ms, int *levels);
+
 /* ---- several GPUs from one host thread (sm_create_group) ----
  * A group holds one handle and one host worker thread per device (devices == NULL: 0..ngpu-1;
  * a device may repeat).  Calls are synchronous, like sm_block_match_u8.

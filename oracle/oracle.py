@@ -27,8 +27,8 @@ _f64p = ctypes.POINTER(ctypes.c_double)
 
 def build(force: bool = False) -> str:
     """Compile the oracle with the committed Makefile (gcc -O2)."""
-    src = os.path.join(_HERE, "bm_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("bm_oracle.c", "st_oracle.c")]
+    if force or not os.path.exists(_LIB_PATH) or any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
@@ -66,6 +66,13 @@ def lib():
         L.ora_guided_probe.restype = ctypes.c_int
         L.ora_box_lr_probe.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
         L.ora_box_lr_probe.restype = ctypes.c_int
+        L.ora_st_cost.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.ora_st_tree.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _i32p, _i32p, _u8p, _i32p, _u8p,
+                                  _u8p]
+        L.ora_st_tree.restype = ctypes.c_int
+        L.ora_st_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                  ctypes.c_float, _u8p]
+        L.ora_st_disp.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -259,6 +266,44 @@ def median(src, r: int):
     out = np.empty((H, W), np.uint8)
     lib().ora_median_u8(_p(src, _u8p), W, H, r, _p(out, _u8p))
     return out
+
+
+def _bgr(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    assert a.ndim == 3 and a.shape[2] == 3
+    return a
+
+
+def st_cost(left_bgr, right_bgr, D: int) -> np.ndarray:
+    """STMatching GetMatchingCost (StereoHelper.cpp:75-129): float [H, W, D] colour + gradient cost."""
+    L, R = _bgr(left_bgr), _bgr(right_bgr)
+    H, W = L.shape[:2]
+    out = np.empty((H, W, D), np.float32)
+    lib().ora_st_cost(_p(L, _u8p), _p(R, _u8p), W, H, D, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return out
+
+
+def st_tree(left_bgr, tau: float = 1200.0):
+    """STMatching BuildSegmentTree with CColorWeight (SegmentTree.cpp:38-139): the tree in BFS order.
+    Returns dict(node, parent, pdist, first, nchild, cdist [P, 4], levels)."""
+    L = _bgr(left_bgr)
+    H, W = L.shape[:2]
+    P = W * H
+    t = dict(node=np.empty(P, np.int32), parent=np.empty(P, np.int32), pdist=np.empty(P, np.uint8),
+             first=np.empty(P, np.int32), nchild=np.empty(P, np.uint8), cdist=np.zeros((P, 4), np.uint8))
+    t["levels"] = lib().ora_st_tree(_p(L, _u8p), W, H, tau, _p(t["node"], _i32p), _p(t["parent"], _i32p),
+                                    _p(t["pdist"], _u8p), _p(t["first"], _i32p), _p(t["nchild"], _u8p),
+                                    _p(t["cdist"], _u8p))
+    return t
+
+
+def st_disp(left_bgr, right_bgr, D: int = 60, scale: int = 4, sigma: float = 0.1, tau: float = 1200.0):
+    """STMatching stereo_disparity_normal (ST-1, StereoDisparity.cpp:57-89); returns (disp, levels)."""
+    L, R = _bgr(left_bgr), _bgr(right_bgr)
+    H, W = L.shape[:2]
+    out = np.empty((H, W), np.uint8)
+    levels = lib().ora_st_disp(_p(L, _u8p), _p(R, _u8p), W, H, D, scale, sigma, tau, _p(out, _u8p))
+    return out, levels
 
 
 def synth_pair(seed: int, W: int, H: int, D: int):

@@ -1,0 +1,58 @@
+"""GPU segment-tree stereo (STMatching ST-1) against the C restatement
+(oracle/st_oracle.c), bit for bit: the cost, the tree and the filter's float operations are done in
+the reference's order, so the maps are identical, not merely close."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def matcher():
+    import gpu_stereo_matching_amd as sm
+    m = sm.BlockMatcher(0, 640, 480, 256)
+    yield m
+    m.close()
+
+
+def test_art_reference_defaults(matcher, oracle):
+    """The bundled Art pair at the app's defaults (max level 60, scale 4, sigma 0.1: main.cpp:49-51)."""
+    g = np.load(os.path.join(GOLDEN, "middlebury_bgr.npz"))
+    L, R = g["Art/view1"], g["Art/view5"]
+    want, levels = oracle.st_disp(L, R, 60, 4, 0.1)
+    got = matcher.segment_tree(L, R)
+    assert np.array_equal(got, want), int((got != want).sum())
+    tree_ms, total_ms, lv = matcher.segment_tree_stats()
+    assert lv == levels and 0 < tree_ms < total_ms
+
+
+@pytest.mark.parametrize("W,H,D,scale,sigma,seed", [(97, 61, 16, 1, 0.1, 1), (2, 5, 3, 4, 0.1, 2),
+                                                     (300, 200, 64, 2, 0.08, 3), (123, 1, 9, 3, 0.5, 4),
+                                                     (64, 48, 80, 3, 0.005, 5)])
+def test_random_pairs(matcher, oracle, W, H, D, scale, sigma, seed):
+    """Textured and flat random BGR pairs (a right view shifted by a known disparity, plus flat
+    patches that produce long equal-weight edge runs), odd sizes, a 1-row frame, sigma below the
+    reference's 0.01 clamp."""
+    rng = np.random.default_rng(seed)
+    L = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    L[: H // 2, : W // 3] = 77
+    R = np.roll(L, -min(5, W - 1), axis=1)
+    R[:, -3:] = rng.integers(0, 256, (H, min(3, W), 3), dtype=np.uint8)
+    want, _ = oracle.st_disp(L, R, D, scale, sigma)
+    got = matcher.segment_tree(L, R, D, scale, sigma)
+    assert np.array_equal(got, want), int((got != want).sum())
+
+
+def test_argument_errors(matcher):
+    import gpu_stereo_matching_amd as sm
+    a = np.zeros((4, 1, 3), np.uint8)
+    with pytest.raises(sm.SMError):
+        matcher.segment_tree(a, a)                       # width 1: the gradient needs two columns
+    b = np.zeros((4, 4, 3), np.uint8)
+    with pytest.raises(sm.SMError):
+        matcher.segment_tree(b, b, 0)
+    with pytest.raises(sm.SMError):
+        matcher.segment_tree(b, b, 8, 4, 0.0)

@@ -181,3 +181,38 @@ def test_guided_probe_matches_volume_oracle(oracle):
     assert np.array_equal(out, disp) and np.array_equal(b2, best) and np.array_equal(bR, bestr)
     assert np.array_equal(qL, q[disp.astype(int), ys, xs])
     assert np.array_equal(qR, cr[probe_r.astype(int), ys, xs])
+
+
+def test_st_tree_invariants(oracle):
+    """The restated segment tree (SegmentTree.cpp:38-139) is a BFS-ordered spanning tree of the pixel grid:
+    a permutation of the pixels, parents before children, each node's children a contiguous BFS run whose
+    parent is that node, and tree edges between 4-neighbours only."""
+    rng = np.random.default_rng(7)
+    H, W = 30, 40
+    L = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    L[5:20, 3:25] = 120                              # a flat segment: many equal-weight edges
+    t = oracle.st_tree(L)
+    P = H * W
+    assert t["levels"] > 1
+    assert sorted(t["node"].tolist()) == list(range(P)) and t["node"][0] == 0 and t["parent"][0] == -1
+    for i in range(1, P):
+        p = t["parent"][i]
+        assert 0 <= p < i
+        a, b = t["node"][i], t["node"][p]
+        assert abs(a - b) in (1, W) and (abs(a - b) == W or a // W == b // W)
+    for i in range(P):
+        for z in range(t["nchild"][i]):
+            c = t["first"][i] + z
+            assert t["parent"][c] == i and t["pdist"][c] == t["cdist"][i, z]
+
+
+def test_st_recovers_shift(oracle):
+    """ST-1 on a textured pair shifted by 7 pixels: the disparity (scale 1) is 7 nearly everywhere
+    right of the first columns (where x < 7 has no match)."""
+    rng = np.random.default_rng(3)
+    H, W, s = 80, 120, 7
+    base = rng.integers(0, 256, (H, W + s, 3), dtype=np.uint8)
+    L, R = base[:, :W].copy(), base[:, s:].copy()    # L(x) = R(x - s)
+    d, levels = oracle.st_disp(L, R, 16, 1, 0.1)
+    assert levels > 0
+    assert (d[:, 12:] == s).mean() > 0.97

@@ -10,7 +10,7 @@ OUT=tools/ab/$NAME
 mkdir -p $OUT
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wall -Wno-unused-result $EXTRA"
 pids=()
-for f in sm_capi bm_box bm_aux bm_guided bm_pre bm_post bm_volume bm_staged bm_rectify; do
+for f in sm_capi bm_box bm_aux bm_guided bm_segtree bm_pre bm_post bm_volume bm_staged bm_rectify; do
   /opt/rocm/bin/hipcc $FLAGS -c $SRC/$f.hip -o $OUT/$f.o &
   pids+=($!)
 done
