@@ -298,7 +298,8 @@ class BlockMatcher:
         return u.value, m.value, d.value
 
     def staged_kernel_ms(self) -> Tuple[float, float, float]:
-        """(AD volume, SAD volume, WTA) kernel ms of the last frame of the last 'box-staged' pass."""
+        """(AD volume, SAD volume, WTA) kernel ms per frame of the last launch group (up to 8 frames) of the
+        last 'box-staged' pass."""
         a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         _capi.check(self._lib.sm_last_staged_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value

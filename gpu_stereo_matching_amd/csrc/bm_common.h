@@ -63,8 +63,9 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
                             int D, uint8_t* dif, int64_t dstride, hipStream_t s);
 // staged box path (bm_staged.hip): u16 SAD volume from the AD volume, and WTA over the SAD volume
 hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, int D, uint16_t* sad, hipStream_t s);
-hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, uint32_t seed_key, uint8_t* disp,
-                             int out_pitch, hipStream_t s);
+// (`frames` consecutive frames of D planes each; frame f's map at disp + f * out_stride)
+hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,
+                             int out_pitch, int64_t out_stride, hipStream_t s);
 // (2r+1)^2 median with replicate borders, radius 1..3 (bm_post.hip)
 hipError_t launch_median(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch, int radius,
                          uint8_t* dst, int dpitch, int64_t dstride, hipStream_t s);

@@ -18,17 +18,31 @@ namespace {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kST = 256;
-constexpr int kSC = 4 * kST;       // K2: input columns per strip (4 per thread)
+// K2 build switches (same-box A/B, 8 x 1080p D=128 frames per launch, tools/ab_staged_kernels.py):
+//   SM_SAD_CPT 8 vs 4 columns per thread (16-B vs 8-B stores): 162 vs 188 us per frame;
+//   SM_SAD_NT nontemporal SAD stores: the WTA that reads them back runs 81 vs 93 us;
+//   SM_SAD_BLOCKS 16384 vs 2048 / 4096 / 8192: 156 vs 169 / 163 / 164 us.
+#ifndef SM_SAD_CPT
+#define SM_SAD_CPT 8
+#endif
+#ifndef SM_SAD_NT
+#define SM_SAD_NT 1
+#endif
+constexpr int kCPT = SM_SAD_CPT;    // K2: input (and output) columns per thread, 4 or 8
+constexpr int kSC = kCPT * kST;     // K2: input columns per strip
 constexpr int kSO = kSC - 16;      // K2: output columns per strip (the strip starts 8 columns early)
-constexpr int kSadBlocks = 4096;  // K2 blocks per launch (2048 measured 10 % slower, 8192 the same)
-constexpr int kSadRowsPerSync = 1; // K2 output rows staged in LDS per workgroup barrier (4 measured 2 % slower)
+#ifndef SM_SAD_BLOCKS
+#define SM_SAD_BLOCKS 16384
+#endif
+constexpr int kSadBlocks = SM_SAD_BLOCKS;  // K2 blocks per launch (>= 32-row bands)
+static_assert(kCPT == 4 || kCPT == 8, "K2 columns per thread");
 
-// K2: one column strip x one row band of one d plane per block.  A thread owns 4 input columns
-// and walks the band's rows once: vertical window sums run in registers (two packed u16 pairs,
-// the rows leaving the window kept in a register ring of 2r+1 dwords), each output row's
-// vertical sums go to LDS, and each thread forms 4 horizontal window sums from its neighbours'
-// columns.  Every AD byte is read once per band (the 2r halo rows of a band are re-read;
-// >= ~64-row bands), every SAD value written once as part of an 8-B store.
+// K2: one column strip x one row band of one d plane per block.  A thread owns kCPT input columns
+// and walks the band's rows once: vertical window sums run in registers (packed u16 pairs, the
+// rows leaving the window kept in a register ring of 2r+1 words), each output row's vertical sums
+// go to LDS, and each thread forms kCPT horizontal window sums from its neighbours' columns.
+// Every AD byte is read once per band (the 2r halo rows of a band are re-read; >= ~64-row bands),
+// every SAD value written once as part of a 2*kCPT-byte store.
 __device__ __forceinline__ uint32_t ld4z(const uint8_t* plane, int y, int x, int W, int H) {
     if (y < 0 || y >= H) return 0u;
     const uint8_t* row = plane + (int64_t)y * W;
@@ -44,12 +58,31 @@ __device__ __forceinline__ uint32_t ld4z(const uint8_t* plane, int y, int x, int
     return v;
 }
 
+template <int N>
+struct Words {
+    uint32_t w[N];
+};
+
+// kCPT / 4 dwords of row y from column x (bytes outside the plane read as 0)
+__device__ __forceinline__ Words<kCPT / 4> ldz(const uint8_t* plane, int y, int x, int W, int H) {
+    Words<kCPT / 4> r;
+    if constexpr (kCPT == 8) {
+        if (y >= 0 && y < H && x >= 0 && x + 7 < W) {
+            __builtin_memcpy(r.w, plane + (int64_t)y * W + x, 8);
+            return r;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < kCPT / 4; ++g) r.w[g] = ld4z(plane, y, x + 4 * g, W, H);
+    return r;
+}
+
 template <int R>
 __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict__ ad, int W, int H, int rows_per_band,
                                                       int bands, int strips, uint16_t* __restrict__ sad) {
     constexpr int K = 2 * R + 1;
-    constexpr int RB = kSadRowsPerSync;
-    __shared__ __attribute__((aligned(16))) uint16_t vs[2][RB][kSC + 16];
+    constexpr int NG = kCPT / 4;                        // 4-column groups per thread
+    __shared__ __attribute__((aligned(16))) uint16_t vs[2][kSC + 16];
     const int t = threadIdx.x;
     // XCD-aware order: each XCD walks a contiguous run of (plane, strip, band) ids, band fastest,
     // so the 2r halo rows a band shares with the band above are still in that XCD's L2
@@ -62,73 +95,98 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
     const uint8_t* plane = ad + (int64_t)d * P;
     uint16_t* outp = sad + (int64_t)d * P;
     const int xs = sx * kSO;                            // first output column of the strip
-    const int xin = xs - 8 + 4 * t;                     // this thread's 4 input columns
-    const bool vec_out = ((W & 3) == 0) && ((reinterpret_cast<uintptr_t>(sad) & 7) == 0);
-    const int x = xs + 4 * t;
-    const bool out_on = 4 * t < kSO && x < W;
-    // vertical sums: E = (col0, col2), O = (col1, col3) as u16 pairs (<= (2r+1) * 255)
-    uint32_t E = 0u, O = 0u, ring[K];
+    const int xin = xs - 8 + kCPT * t;                  // this thread's kCPT input columns
+    const bool vec_out = (W % kCPT == 0) && ((reinterpret_cast<uintptr_t>(sad) & (2 * kCPT - 1)) == 0);
+    const int x = xs + kCPT * t;
+    const bool out_on = kCPT * t < kSO && x < W;
+    // vertical sums of group g: E = (col0, col2), O = (col1, col3) as u16 pairs (<= (2r+1) * 255)
+    uint32_t E[NG], O[NG], ring[K][NG];
 #pragma unroll
-    for (int j = 0; j < K; ++j) ring[j] = 0u;
+    for (int g = 0; g < NG; ++g) {
+        E[g] = O[g] = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j) ring[j][g] = 0u;
+    }
     const int yi_end = yo1 + R;                         // input rows [yo0 - R, yo1 + R)
-    int buf = 0, nrow = 0, yfirst = yo0;
-    // horizontal sums of the nrow rows staged in vs[buf] (rows yfirst ..), behind one barrier
-    auto flush = [&]() {
+    int buf = 0;
+    // horizontal sums of output row y, staged in vs[buf], behind one barrier
+    auto flush = [&](int y) {
         __syncthreads();
-        for (int q = 0; q < nrow; ++q) {
-            const uint16_t* row = vs[buf][q];
-            // outputs xs + 4t + k (k < 4): window of vs indices [4t + 8 + k - R, 4t + 8 + k + R]
-            uint32_t w[12];
+        const uint16_t* row = vs[buf];
+        // outputs xs + kCPT t + k (k < kCPT): window of vs indices [kCPT t + 8 + k - R, kCPT t + 8 + k + R]
+        constexpr int NW2 = (kCPT + 16) / 4;            // 8-B reads covering kCPT + 16 u16
+        uint32_t w[2 * NW2];
 #pragma unroll
-            for (int u = 0; u < 6; ++u) {
-                const uint2 x2 = *reinterpret_cast<const uint2*>(row + 4 * t + 4 * u);
-                w[2 * u] = x2.x;
-                w[2 * u + 1] = x2.y;
-            }
-            auto val = [&](int i) -> uint32_t { return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu); };
-            uint32_t sum = 0;
+        for (int u = 0; u < NW2; ++u) {
+            const uint2 x2 = *reinterpret_cast<const uint2*>(row + kCPT * t + 4 * u);
+            w[2 * u] = x2.x;
+            w[2 * u + 1] = x2.y;
+        }
+        auto val = [&](int i) -> uint32_t { return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu); };
+        uint32_t sum = 0;
 #pragma unroll
-            for (int i = 8 - R; i <= 8 + R; ++i) sum += val(i);
-            uint32_t res[4];
-            res[0] = sum;
+        for (int i = 8 - R; i <= 8 + R; ++i) sum += val(i);
+        uint32_t res[kCPT];
+        res[0] = sum;
 #pragma unroll
-            for (int k = 1; k < 4; ++k) {
-                sum += val(8 + R + k) - val(8 - R + k - 1);
-                res[k] = sum;                           // <= (2r+1)^2 * 255 < 2^16 for r <= 7
-            }
-            if (out_on) {
-                uint16_t* dst = outp + (int64_t)(yfirst + q) * W + x;
-                if (vec_out && x + 4 <= W) {
-                    *reinterpret_cast<uint2*>(dst) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+        for (int k = 1; k < kCPT; ++k) {
+            sum += val(8 + R + k) - val(8 - R + k - 1);
+            res[k] = sum;                               // <= (2r+1)^2 * 255 < 2^16 for r <= 7
+        }
+        if (out_on) {
+            uint16_t* dst = outp + (int64_t)y * W + x;
+            if (vec_out && x + kCPT <= W) {
+                if constexpr (kCPT == 8) {
+                    const u32x4 v = {res[0] | (res[1] << 16), res[2] | (res[3] << 16), res[4] | (res[5] << 16),
+                                     res[6] | (res[7] << 16)};
+                    if (SM_SAD_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+                    else *reinterpret_cast<u32x4*>(dst) = v;
                 } else {
-                    for (int k = 0; k < 4 && x + k < W; ++k) dst[k] = (uint16_t)res[k];
+                    const uint2 v = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+                    if (SM_SAD_NT) {
+                        __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(dst));
+                        __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(dst) + 1);
+                    } else {
+                        *reinterpret_cast<uint2*>(dst) = v;
+                    }
                 }
+            } else {
+                for (int k = 0; k < kCPT && x + k < W; ++k) dst[k] = (uint16_t)res[k];
             }
         }
-        buf ^= 1;                                       // the next rows go to the other buffer
-        yfirst += nrow;
-        nrow = 0;
+        buf ^= 1;                                       // the next row goes to the other buffer
     };
     for (int base = yo0 - R; base < yi_end; base += K) {
         // ring slot j holds row base + j - K (this loop's row base + j replaces it)
-        uint32_t nw[K];
+        Words<NG> nw[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) nw[j] = (base + j < yi_end) ? ld4z(plane, base + j, xin, W, H) : 0u;
+        for (int j = 0; j < K; ++j) {
+            if (base + j < yi_end) {
+                nw[j] = ldz(plane, base + j, xin, W, H);
+            } else {
+#pragma unroll
+                for (int g = 0; g < NG; ++g) nw[j].w[g] = 0u;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const int yi = base + j;
             if (yi >= yi_end) break;                    // block-uniform
-            const uint32_t v = nw[j], o = ring[j];
-            ring[j] = v;
-            E += (v & 0x00FF00FFu) - (o & 0x00FF00FFu);
-            O += ((v >> 8) & 0x00FF00FFu) - ((o >> 8) & 0x00FF00FFu);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t v = nw[j].w[g], o = ring[j][g];
+                ring[j][g] = v;
+                E[g] += (v & 0x00FF00FFu) - (o & 0x00FF00FFu);
+                O[g] += ((v >> 8) & 0x00FF00FFu) - ((o >> 8) & 0x00FF00FFu);
+            }
             if (yi - R < yo0) continue;                 // warm-up rows of the band (window centred on yi - R)
-            *reinterpret_cast<uint2*>(&vs[buf][nrow][4 * t]) =
-                make_uint2(__builtin_amdgcn_perm(O, E, 0x05040100u), __builtin_amdgcn_perm(O, E, 0x07060302u));
-            if (++nrow == RB) flush();
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+                *reinterpret_cast<uint2*>(&vs[buf][kCPT * t + 4 * g]) =
+                    make_uint2(__builtin_amdgcn_perm(O[g], E[g], 0x05040100u), __builtin_amdgcn_perm(O[g], E[g], 0x07060302u));
+            flush(yi - R);
         }
     }
-    if (nrow) flush();
 }
 
 // K3: 8 pixels per thread, one 16-B nontemporal load per d plane (the volume is streamed once and
@@ -138,7 +196,7 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
 // thread groups of one workgroup (same pixels, consecutive d ranges), merged through LDS in d order:
 // SPLIT times the workgroups of a one-group-per-pixel-block grid, for the same bytes per thread.
 #ifndef SM_WTA_UNROLL
-#define SM_WTA_UNROLL 8
+#define SM_WTA_UNROLL 16   // 8-frame launches: 81.4 us per frame vs 93.5 for 8 (with nontemporal SAD stores)
 #endif
 #ifndef SM_WTA_SPLIT
 #define SM_WTA_SPLIT 4   // 1080p D=128 same-box A/B: 102.6 us (1 group), 99.2 (4 groups)
@@ -150,8 +208,11 @@ constexpr int kWtaSplit = SM_WTA_SPLIT;
 
 __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restrict__ sad, int W, int H, int D,
                                                          uint32_t seed_key, uint8_t* __restrict__ disp,
-                                                         int out_pitch) {
+                                                         int out_pitch, int64_t out_stride) {
     constexpr int NPX = 8;
+    // frame blockIdx.y of the launch group: its D planes follow the previous frame's
+    sad += (int64_t)blockIdx.y * D * ((int64_t)W * H);
+    disp += (int64_t)blockIdx.y * out_stride;
     constexpr int TPG = kST / kWtaSplit;             // threads per d group
     __shared__ uint32_t part[kWtaSplit > 1 ? kWtaSplit - 1 : 1][TPG][NPX + 1];
     const int64_t P = (int64_t)W * H;
@@ -260,13 +321,13 @@ hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, in
 #undef SM_BOX_SAD_CASE
 }
 
-hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, uint32_t seed_key, uint8_t* disp,
-                             int out_pitch, hipStream_t s) {
+hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,
+                             int out_pitch, int64_t out_stride, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
     const int64_t blocks = (P + 8 * (kST / kWtaSplit) - 1) / (8 * (kST / kWtaSplit));
-    if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(volume_wta_kernel, dim3((unsigned)blocks), dim3(kST), 0, s, sad, W, H, D, seed_key, disp,
-                       out_pitch);
+    if (blocks <= 0 || blocks > 0x7FFFFFFF || frames <= 0 || frames > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(volume_wta_kernel, dim3((unsigned)blocks, (unsigned)frames), dim3(kST), 0, s, sad, W, H, D,
+                       seed_key, disp, out_pitch, out_stride);
     return hipGetLastError();
 }
 

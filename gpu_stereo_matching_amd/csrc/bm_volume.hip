@@ -17,7 +17,7 @@ namespace {
 
 constexpr int kVT = 256;
 #ifndef SM_ADV_BLOCKS
-#define SM_ADV_BLOCKS 4096
+#define SM_ADV_BLOCKS 16384   // 8-frame staged launches: 52.6 us per frame vs 55.6 at 4096
 #endif
 #ifndef SM_ADV_MAXSPLIT
 #define SM_ADV_MAXSPLIT 16

@@ -8,6 +8,7 @@
 //     (the reference never checks, so its W > 1024 launch failure returns all zeros, :253);
 //   * any frame size works (the reference's fixed (8,10,D)x(32,32) grid covers 320x256 only, :231-233).
 #include <dlfcn.h>
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <cstdio>
@@ -71,8 +72,10 @@ struct sm_handle {
     sm::StStats st_stats;
     float st_total_ms = 0.f;
     bool st_valid = false;
-    // staged box path: events around the last frame's AD / SAD / WTA kernels (sm_last_staged_kernel_ms)
+    // staged box path: events around the last launch group's AD / SAD / WTA kernels
+    // (sm_last_staged_kernel_ms reports them per frame of that group)
     hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int kev_frames = 1;
     bool kev_valid = false;
 };
 
@@ -173,30 +176,41 @@ int ensure_vol(sm_handle* h, size_t bytes) {
     return SM_OK;
 }
 
-// Staged box path, frame by frame through one AD (u8) + SAD (u16) volume workspace.
+// Staged box path through AD (u8) + SAD (u16) volume workspaces, in launch groups of up to
+// kStagedGroup frames (workspace <= kStagedBytes): one AD, one SAD and one WTA launch per group, as
+// the fused path batches frames per launch.  The SAD launch sees the group's g*D planes as one
+// volume; the WTA launch takes the frame from blockIdx.y.
+constexpr int kStagedGroup = 8;
+constexpr int64_t kStagedBytes = (int64_t)8 << 30;
 int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch, int64_t fstride,
                int radius, int D, bool med, uint8_t* disp, int opitch, int64_t ostride, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
     if (W > 4096) return fail(SM_ERR_INVALID_ARG, "SM_STAGED: width %d exceeds 4096", W);
-    int rc = ensure_vol(h, (size_t)(3 * P * D) + (med ? (size_t)P : 0));
+    const int64_t per_frame = 3 * P * D + (med ? P : 0);
+    int group = (int)std::min<int64_t>(kStagedGroup, std::max<int64_t>(1, kStagedBytes / per_frame));
+    group = std::min(group, std::max(batch, 1));
+    int rc = ensure_vol(h, (size_t)(per_frame * group));
     if (rc) return rc;
     uint8_t* ad = h->d_vol;
-    uint16_t* sad = reinterpret_cast<uint16_t*>(h->d_vol + P * D);
-    uint8_t* raw = h->d_vol + 3 * P * D;
+    uint16_t* sad = reinterpret_cast<uint16_t*>(h->d_vol + group * P * D);
+    uint8_t* raw = h->d_vol + 3 * group * P * D;
     if (!h->kev[0])
         for (auto& e : h->kev) SM_HIP(hipEventCreate(&e));
     h->kev_valid = false;
-    for (int f = 0; f < batch; ++f) {
-        const bool last = f == batch - 1;   // the last frame's kernels are bracketed by events
+    for (int f0 = 0; f0 < batch; f0 += group) {
+        const int g = std::min(group, batch - f0);
+        const bool last = f0 + g >= batch;   // the last group's kernels are bracketed by events
         if (last) SM_HIP(hipEventRecord(h->kev[0], s));
-        SM_HIP(sm::launch_ad_volume(L + f * fstride, R + f * fstride, W, H, pitch, fstride, 1, D, ad, P * D, s));
+        SM_HIP(sm::launch_ad_volume(L + f0 * fstride, R + f0 * fstride, W, H, pitch, fstride, g, D, ad, P * D, s));
         if (last) SM_HIP(hipEventRecord(h->kev[1], s));
-        SM_HIP(sm::launch_box_sad_volume(ad, W, H, radius, D, sad, s));
+        SM_HIP(sm::launch_box_sad_volume(ad, W, H, radius, g * D, sad, s));
         if (last) SM_HIP(hipEventRecord(h->kev[2], s));
-        uint8_t* out = disp + f * ostride;
-        SM_HIP(sm::launch_volume_wta(sad, W, H, D, seed_key(radius), med ? raw : out, med ? W : opitch, s));
+        uint8_t* out = disp + f0 * ostride;
+        SM_HIP(sm::launch_volume_wta(sad, W, H, D, g, seed_key(radius), med ? raw : out, med ? W : opitch,
+                                     med ? P : ostride, s));
         if (last) SM_HIP(hipEventRecord(h->kev[3], s));
-        if (med) SM_HIP(sm::launch_median(raw, W, H, W, P, 1, 3, out, opitch, ostride, s));
+        if (med) SM_HIP(sm::launch_median(raw, W, H, W, P, g, 3, out, opitch, ostride, s));
+        if (last) h->kev_frames = g;
     }
     h->kev_valid = batch > 0;
     return SM_OK;
@@ -730,7 +744,10 @@ SM_API int sm_last_staged_kernel_ms(sm_handle* h, float* ad_ms, float* sad_ms, f
     if (!h->kev_valid) return fail(SM_ERR_INVALID_ARG, "no SM_STAGED pass has run on this handle");
     SM_HIP(hipEventSynchronize(h->kev[3]));
     float t[3];
-    for (int i = 0; i < 3; ++i) SM_HIP(hipEventElapsedTime(&t[i], h->kev[i], h->kev[i + 1]));
+    for (int i = 0; i < 3; ++i) {
+        SM_HIP(hipEventElapsedTime(&t[i], h->kev[i], h->kev[i + 1]));
+        t[i] /= (float)h->kev_frames;
+    }
     if (ad_ms) *ad_ms = t[0];
     if (sad_ms) *sad_ms = t[1];
     if (wta_ms) *wta_ms = t[2];

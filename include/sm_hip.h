@@ -95,8 +95,10 @@ SM_API int sm_block_match_lr_u8(sm_handle *h, const uint8_t *left, const uint8_t
  * (Device.cu:218,238,257,292).  Any pointer may be NULL. */
 SM_API int sm_last_stage_ms(sm_handle *h, float *upload_ms, float *match_ms, float *download_ms);
 
-/* Kernel times (ms, hipEvents on the launch stream) of the last frame of the last SM_STAGED pass:
- * AD volume (kernalPreCal_V2, Device.cu:19-32), SAD volume and WTA (kernalFindCorr's two halves,
+/* Kernel times (ms, hipEvents on the launch stream) of the last SM_STAGED pass, per frame: the
+ * pass runs its frames in launch groups of up to 8 (one AD, one SAD and one WTA launch per group),
+ * and each figure is the last group's launch time divided by its frame count.  AD volume
+ * (kernalPreCal_V2, Device.cu:19-32), SAD volume and WTA (kernalFindCorr's two halves,
  * Device.cu:34-64).  Waits for that pass to finish.  Any pointer may be NULL. */
 SM_API int sm_last_staged_kernel_ms(sm_handle *h, float *ad_ms, float *sad_ms, float *wta_ms);
 

@@ -554,6 +554,21 @@ def test_staged_median_batch(matcher, oracle, torch):
         assert np.array_equal(out[b].cpu().numpy(), oracle.median(oracle.box_disp(pairs[b][0], pairs[b][1], 3, 32), 3))
 
 
+@pytest.mark.parametrize("median", [False, True])
+def test_staged_launch_groups(matcher, oracle, torch, median):
+    """11 frames = launch groups of 8 and 3 (one AD / SAD / WTA launch per group, frames from
+    blockIdx.y in the WTA): every frame equals the fused kernel's map."""
+    pairs = [oracle.synth_pair(500 + b, 241, 67, 48) for b in range(11)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    staged = matcher.match_device(Lt, Rt, 4, 48, agg="box-staged", median=median)
+    fused = matcher.match_device(Lt, Rt, 4, 48, median=median)
+    torch.cuda.synchronize()
+    assert torch.equal(staged, fused)
+    k = matcher.staged_kernel_ms()
+    assert len(k) == 3 and all(t > 0 for t in k)
+
+
 @pytest.mark.parametrize("seed", list(range(40)))
 def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
     """Seeded random shapes / radii / disparity counts / textures: box (host and batched device),

@@ -1,19 +1,23 @@
 """Same-box A/B of the staged kernels' HIP-event times (sm_last_staged_kernel_ms) for several
 libsm_hip.so builds, 1080p D=128 r=5 frames, rounds alternated, one process per library and round.
-usage: python tools/ab_staged_kernels.py lib1.so lib2.so ... [--rounds N]"""
+usage: python tools/ab_staged_kernels.py lib1.so lib2.so ... [--rounds N] [--frames F]
+(F frames per call, default 8 = one launch group; the kernel times are per frame)"""
 import os, statistics, subprocess, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 libs = [a for a in sys.argv[1:] if a.endswith(".so")]
 rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 3
+frames = int(sys.argv[sys.argv.index("--frames") + 1]) if "--frames" in sys.argv else 8
 CODE = """
 import sys; sys.path.insert(0, {root!r})
 import numpy as np, torch, gpu_stereo_matching_amd._capi as C
 C.load({lib!r})
 import gpu_stereo_matching_amd as sm
 m = sm.BlockMatcher(0, 1920, 1080, 256)
-L, R = sm.synth_pair(1234, 1920, 1080, 128)
-Lt, Rt = torch.from_numpy(L[None]).cuda(), torch.from_numpy(R[None]).cuda()
+F = {frames}
+pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(F)]
+Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
 out = torch.empty_like(Lt)
 ref = m.match_device(Lt, Rt, 5, 128, agg='box').cpu().numpy()
 acc = []
@@ -29,7 +33,7 @@ alg = [P * (D + 2), 3 * P * D, 2 * P * D + P]
 res = {l: [] for l in libs}
 for r in range(rounds):
     for l in libs:
-        o = subprocess.run([sys.executable, "-c", CODE.format(root=ROOT, lib=os.path.abspath(l))], capture_output=True,
+        o = subprocess.run([sys.executable, "-c", CODE.format(root=ROOT, lib=os.path.abspath(l), frames=frames)], capture_output=True,
                            text=True, timeout=300)
         line = [x for x in o.stdout.splitlines() if x.startswith("KMS")]
         if not line:
