@@ -272,22 +272,23 @@ def run_variants(sm, torch, dev, stream, seed):
             up, mt, dn = m.stage_ms()
             out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
                          "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
-        # STMatching's segment-tree stereo ST-1 (§8f rank 4) on the bundled Art pair at the app's defaults:
-        # a synchronous host call (host tree build + GPU cost / filter / WTA / median), wall time
+        # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's
+        # defaults: a synchronous host call (host tree builds + GPU cost / filter / WTA / median / LR check), wall
         g = np.load(os.path.join(ROOT, "tests", "golden", "middlebury_bgr.npz"))
         Lb, Rb = g["Art/view1"], g["Art/view5"]
-        for _ in range(2):
-            m.segment_tree(Lb, Rb)
-        ts = []
-        for _ in range(7):
-            t0 = time.perf_counter()
-            m.segment_tree(Lb, Rb)
-            ts.append((time.perf_counter() - t0) * 1000)
-        tree_ms, _, levels = m.segment_tree_stats()
-        ms = float(np.median(ts))
-        out["segment tree ST-1 Art 463x370 d60 (host tree + GPU filter, wall)"] = {
-            "ms_per_frame": round(ms, 3), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
-            "host_tree_ms": round(tree_ms, 3), "tree_levels": levels}
+        for method, label in ((0, "segment tree ST-1 Art 463x370 d60 (host tree + GPU filter, wall)"),
+                              (1, "segment tree ST-2 Art 463x370 d60 (3 host trees + GPU filters + LR check, wall)")):
+            for _ in range(2):
+                m.segment_tree(Lb, Rb, method=method)
+            ts = []
+            for _ in range(7):
+                t0 = time.perf_counter()
+                m.segment_tree(Lb, Rb, method=method)
+                ts.append((time.perf_counter() - t0) * 1000)
+            tree_ms, _, levels = m.segment_tree_stats()
+            ms = float(np.median(ts))
+            out[label] = {"ms_per_frame": round(ms, 3), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
+                          "host_tree_ms": round(tree_ms, 3), "tree_levels": levels}
     finally:
         m.close()
     return out

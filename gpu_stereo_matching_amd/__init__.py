@@ -153,23 +153,30 @@ class BlockMatcher:
                                                     num_disp, _flags(agg, lr_check), out.ctypes.data, W))
         return out
 
-    def segment_tree(self, left_bgr, right_bgr, max_level: int = 60, scale: int = 4, sigma: float = 0.1) -> np.ndarray:
-        """STMatching's segment-tree stereo, ST-1 (stereo_disparity_normal, StereoDisparity.cpp:57-89):
-        HxWx3 uint8 BGR frames -> colour + gradient cost over d < max_level -> tree aggregation on the
-        left view's colour tree -> WTA -> 7x7 median -> x scale.  Cost, filter, WTA and median on the GPU,
-        the tree on the host (as the reference).  Defaults as STMatching/main.cpp:49-51."""
+    def segment_tree(self, left_bgr, right_bgr, max_level: int = 60, scale: int = 4, sigma: float = 0.1,
+                     method: int = 0) -> np.ndarray:
+        """STMatching's segment-tree stereo on HxWx3 uint8 BGR frames, `method` as STMatching/main.cpp's
+        7th argument (defaults as its :49-52):
+          0 = ST-1 (stereo_disparity_normal, StereoDisparity.cpp:57-89): colour + gradient cost over
+              d < max_level -> tree aggregation on the left view's colour tree -> WTA -> 7x7 median -> x scale;
+          1 = ST-2 (stereo_disparity_iteration, :91-160): first-pass left / right maps on colour trees of
+              each view, the left-right check, then a colour + depth tree on the left view.
+        Cost, filter, WTA, median and LR check on the GPU, the trees on the host (as the reference)."""
         Lb = np.ascontiguousarray(left_bgr, dtype=np.uint8)
         Rb = np.ascontiguousarray(right_bgr, dtype=np.uint8)
         if Lb.ndim != 3 or Lb.shape[2] != 3 or Lb.shape != Rb.shape:
             raise ValueError("expected two equal HxWx3 uint8 BGR frames")
+        if method not in (0, 1):
+            raise ValueError(f"method must be 0 (ST-1) or 1 (ST-2), got {method}")
         H, W, _ = Lb.shape
         out = np.empty((H, W), np.uint8)
-        _capi.check(self._lib.sm_segment_tree_match_bgr_u8(self._h, Lb.ctypes.data, Rb.ctypes.data, W, H, 3 * W,
-                                                           max_level, scale, sigma, out.ctypes.data, W))
+        fn = self._lib.sm_segment_tree_refined_bgr_u8 if method else self._lib.sm_segment_tree_match_bgr_u8
+        _capi.check(fn(self._h, Lb.ctypes.data, Rb.ctypes.data, W, H, 3 * W, max_level, scale, sigma,
+                       out.ctypes.data, W))
         return out
 
     def segment_tree_stats(self) -> Tuple[float, float, int]:
-        """(host tree-build ms, whole-call ms, BFS levels of the tree) of the last segment_tree call."""
+        """(host tree-build ms, whole-call ms, BFS levels of the last tree) of the last segment_tree call."""
         t, a, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
         _capi.check(self._lib.sm_last_segment_tree_stats(self._h, ctypes.byref(t), ctypes.byref(a), ctypes.byref(n)))
         return t.value, a.value, n.value

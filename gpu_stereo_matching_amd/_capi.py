@@ -37,7 +37,8 @@ EXPORTED = (
     "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
-    "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_last_segment_tree_stats",
+    "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_segment_tree_refined_bgr_u8",
+    "sm_last_segment_tree_stats",
 )
 
 
@@ -96,6 +97,7 @@ def load(path: str = LIB_PATH):
     L.sm_remap_u8_device.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i, vp]
     L.sm_block_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
     L.sm_segment_tree_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, ctypes.c_float, vp, i]
+    L.sm_segment_tree_refined_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, ctypes.c_float, vp, i]
     L.sm_last_segment_tree_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                              ctypes.POINTER(ctypes.c_int)]
     L.sm_stereo_rectify.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp]

@@ -1,4 +1,4 @@
-// bm_segtree.h — segment-tree aggregation (STMatching ST-1) on the GPU: internal interface.
+// bm_segtree.h — segment-tree aggregation (STMatching ST-1 and ST-2) on the GPU: internal interface.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -8,20 +8,21 @@ namespace sm {
 
 // Device workspace of segment_tree_match, owned by a handle, grown on demand.
 struct StWorkspace {
-    uint8_t* w8 = nullptr;     // 3P: edge weights (2P), then the unfiltered map
+    uint8_t* w8 = nullptr;     // ST-1 3P: edge weights (2P), then the unfiltered map; ST-2 10P: both views'
+                               // weights (4P), then the pass maps, the checked map and the mask
     float* grad = nullptr;     // 2P: gradients of both views
-    float* vol = nullptr;      // 2PD: cost / leaf-to-root sums, filtered cost ([D][P], BFS order)
-    int* tree_i = nullptr;     // 5P + 2: rank, parent, first, child, level offsets
-    uint8_t* tree_b = nullptr; // P: distance to the parent
-    float* table = nullptr;    // 256: exp(-i / (255 sigma))
+    float* vol = nullptr;      // ST-1 2PD, ST-2 4PD: cost / leaf-to-root sums, filtered cost ([D][P], BFS order)
+    int* tree_i = nullptr;     // (5P + 2) per tree: rank, parent, first, child, level offsets
+    uint8_t* tree_b = nullptr; // P per tree: distance to the parent
+    float* table = nullptr;    // 256 per tree: exp(-i / (255 sigma))
     size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0;
     ~StWorkspace();
     void release();
 };
 
 struct StStats {
-    int levels = 0;        // BFS levels of the tree
-    float tree_ms = 0.f;   // host time of the tree build
+    int levels = 0;        // BFS levels of the (last) tree
+    float tree_ms = 0.f;   // host time of the tree builds
 };
 
 // stereo_disparity_normal (StereoDisparity.cpp:57-89) on device BGR frames (3 bytes per pixel, row
@@ -29,5 +30,12 @@ struct StStats {
 // Synchronous on stream s (the tree is built on the host from the GPU's edge weights).
 hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch, int D,
                               int scale, float sigma, float tau, uint8_t* d_out, hipStream_t s, StStats* st);
+
+// stereo_disparity_iteration, ST-2 (StereoDisparity.cpp:91-160), same arguments: first-pass left and
+// right maps on colour trees of each view (sigma SIGMA_ONE = 0.08, Toolkit.h:35), the left-right check,
+// then a colour + depth tree (CColorDepthWeight) on the left view with `sigma`.
+hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch,
+                                      int D, int scale, float sigma, float tau, uint8_t* d_out, hipStream_t s,
+                                      StStats* st);
 
 }  // namespace sm

@@ -1,5 +1,6 @@
 // bm_segtree.hip — segment-tree cost aggregation: the reference's STMatching ST-1
-// pipeline (stereo_disparity_normal, StereoDisparity.cpp:57-89) with its O(P*D) parts on the GPU.
+// pipeline (stereo_disparity_normal, StereoDisparity.cpp:57-89) and ST-2 (stereo_disparity_iteration,
+// :91-160) with their O(P*D) parts on the GPU.
 //
 //   guide + edge weights  GPU: 3x3 median of each BGR channel of the left view (MeanFilter(img, 1)
 //                         = ctmf, SegmentTree.cpp:185), max channel |diff| to the right / upper
@@ -18,10 +19,16 @@
 //   WTA, x scale, median  GPU: first d with the smallest cost (StereoHelper.cpp:131-154), times scale
 //                         (saturated; a non-decreasing map commutes with the median), then the 7x7
 //                         median (MeanFilter(disparity, 3), bm_post.hip)
-// The map is bit-exact with the restated oracle (oracle/st_oracle.c).
+// ST-2 adds: the right view's cost taken from the left's (GetRightMatchingCostFromLeft,
+// StereoHelper.cpp:156-180: C_R(y, x, d) = C(y, min(x + d, W - 1), min(d, W - 1 - x)), computed directly),
+// a colour tree of each view filtered in one launch, the left-right check (bm_aux.hip), and a colour +
+// depth tree (CColorDepthWeight, SegmentTree.cpp:196-219) whose float weights the host forms from the
+// colour weights, the first left map and the mask, and orders by a stable radix sort of their bits.
+// The maps are bit-exact with the restated oracle (oracle/st_oracle.c).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <thread>
 #include <vector>
 
 #include "bm_common.h"
@@ -98,7 +105,10 @@ __global__ __launch_bounds__(kST) void st_gradient_kernel(const uint8_t* __restr
 }
 
 // GetMatchingCost (StereoHelper.cpp:75-129) into C[d][rank[p]]; right pixels left of column 0 repeat
-// column 0 (:107-110); double arithmetic as the reference's, rounded to float once
+// column 0 (:107-110); double arithmetic as the reference's, rounded to float once.  RIGHT: the right
+// view's cost at pixel p = (y, x), GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180): the left
+// cost at (y, min(x + d, W - 1)) and disparity min(d, W - 1 - x), whose right pixel is (y, x) itself.
+template <bool RIGHT>
 __global__ __launch_bounds__(kST) void st_cost_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                       int W, int H, int pitch, const float* __restrict__ gL,
                                                       const float* __restrict__ gR, const int* __restrict__ rank, int D,
@@ -107,37 +117,61 @@ __global__ __launch_bounds__(kST) void st_cost_kernel(const uint8_t* __restrict_
     const int x = blockIdx.x * kST + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
     const int64_t P = (int64_t)W * H, p = (int64_t)y * W + x;
-    const uint8_t* l = L + (int64_t)y * pitch + 3 * x;
-    const int lb = l[0], lg = l[1], lr = l[2];
-    const float gl = gL[p];
     const int i = rank[p];
     const double wc = 0.11, wg = 1.0 - wc;
-    for (int d = 0; d < D; ++d) {
-        const int xs = x >= d ? x - d : 0;
-        const uint8_t* r = R + (int64_t)y * pitch + 3 * xs;
-        double cc = (double)(abs(lb - r[0]) + abs(lg - r[1]) + abs(lr - r[2]));
+    auto cost = [&](int xl, int xr) -> float {
+        const uint8_t* l = L + (int64_t)y * pitch + 3 * xl;
+        const uint8_t* r = R + (int64_t)y * pitch + 3 * xr;
+        double cc = (double)(abs(l[0] - r[0]) + abs(l[1] - r[1]) + abs(l[2] - r[2]));
         cc = cc / 3 < 7.0 ? cc / 3 : 7.0;
-        double cg = fabsf(gl - gR[(int64_t)y * W + xs]);
+        double cg = fabsf(gL[(int64_t)y * W + xl] - gR[(int64_t)y * W + xr]);
         cg = cg < 2.0 ? cg : 2.0;
-        C[(int64_t)d * P + i] = (float)(wc * cc + wg * cg);
+        return (float)(wc * cc + wg * cg);
+    };
+    for (int d = 0; d < D; ++d) {
+        const float c = RIGHT ? cost(min(x + d, W - 1), x) : cost(x, x >= d ? x - d : 0);
+        C[(int64_t)d * P + i] = c;
     }
 }
 
-// Filter (SegmentTree.cpp:148-181) of disparity d = blockIdx.x.  C (in: cost, out: the leaf-to-root
-// sums, the reference's costBuffer) and F (out: the filtered cost) are [D][P] in BFS order; levels
-// are the BFS position ranges [lev[l], lev[l + 1]).
-__global__ __launch_bounds__(1024) void st_filter_kernel(float* __restrict__ C, float* __restrict__ F,
-                                                         const int* __restrict__ parent,
-                                                         const uint8_t* __restrict__ pdist,
-                                                         const int* __restrict__ first,
-                                                         const uint32_t* __restrict__ child, const int* __restrict__ lev,
-                                                         int nlev, int P, const float* __restrict__ table_g) {
+// One tree's filter input: C (in: cost, out: the leaf-to-root sums, the reference's costBuffer) and F
+// (out: the filtered cost) are [D][P] in that tree's BFS order; levels are the BFS position ranges
+// [lev[l], lev[l + 1]).
+struct FilterJob {
+    float* C;
+    float* F;
+    const int* parent;
+    const uint8_t* pdist;
+    const int* first;
+    const uint32_t* child;
+    const int* lev;
+    int nlev;
+    const float* table;
+};
+struct FilterJobs {
+    FilterJob j[2];
+};
+
+// Filter (SegmentTree.cpp:148-181) of disparity d = blockIdx.x of job blockIdx.y (ST-2 filters the left
+// and right views' volumes in one launch: each job has only D workgroups).
+#ifndef SM_ST_FILTER_THREADS
+#define SM_ST_FILTER_THREADS 1024
+#endif
+constexpr int kFT = SM_ST_FILTER_THREADS;
+__global__ __launch_bounds__(kFT) void st_filter_kernel(FilterJobs jobs, int P) {
 #pragma clang fp contract(off)
+    const FilterJob& jb = jobs.j[blockIdx.y];
+    const int* __restrict__ parent = jb.parent;
+    const uint8_t* __restrict__ pdist = jb.pdist;
+    const int* __restrict__ first = jb.first;
+    const uint32_t* __restrict__ child = jb.child;
+    const int* __restrict__ lev = jb.lev;
+    const int nlev = jb.nlev;
     __shared__ float table[256];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) table[k] = table_g[k];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) table[k] = jb.table[k];
     __syncthreads();
-    float* U = C + (int64_t)blockIdx.x * P;
-    float* Fd = F + (int64_t)blockIdx.x * P;
+    float* __restrict__ U = jb.C + (int64_t)blockIdx.x * P;
+    float* __restrict__ Fd = jb.F + (int64_t)blockIdx.x * P;
     // leaf to root: a node adds its children in order, each term multiplied then added
     for (int l = nlev - 1; l >= 0; --l) {
         const int lo = lev[l], hi = lev[l + 1];
@@ -188,16 +222,22 @@ __global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F
 }
 
 // ---- host: the tree (sequential, as the reference's) ----
+// disjoint-set.h's forest as separate arrays: find walks only the parent array (a packed 16-B record
+// per element measured 25 % slower on the Art tree)
 struct Dsu {
     std::vector<int> p, rank, size;
     explicit Dsu(int n) : p(n), rank(n, 0), size(n, 1) {
         for (int i = 0; i < n; ++i) p[i] = i;
     }
-    int find(int x) {   // disjoint-set.h:58-64: walk to the root, then point x at it
-        int y = x;
-        while (y != p[y]) y = p[y];
-        p[x] = y;
-        return y;
+    // disjoint-set.h:58-64 walks to the root and points x at it.  Path halving here: compression moves
+    // only non-root parent pointers, so every root, rank and size (all that join and segment_graph
+    // read) is the reference's; the walks are shorter.
+    int find(int x) {
+        while (x != p[x]) {
+            p[x] = p[p[x]];
+            x = p[x];
+        }
+        return x;
     }
     void join(int x, int y) {   // disjoint-set.h:66-82
         if (x != p[x]) x = find(x);
@@ -220,28 +260,59 @@ struct HostTree {
     std::vector<uint32_t> child;
 };
 
-bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
-    const int P = W * H;
-    // edges sorted by (weight, b, a): for a given b the candidates are (a = b-1, right edge of b-1)
-    // and (a = b+W, upper edge of b+W), in that a order; a counting sort by weight filled in b order
-    // is therefore the reference's std::sort order exactly
-    struct E {
-        int a, b;
-        float w;
-    };
+struct Edge {
+    int a, b;
+    float w;
+};
+
+// Every edge of SegmentTree.cpp:44-62 in increasing b, and for one b in increasing a: (b-1, b) is the
+// right edge of b-1 (weight wr[b-1]) and (b+W, b) the upper edge of b+W (weight wu[b+W]).
+template <class F>
+void each_edge(int W, int P, F&& f) {
+    for (int b = 0; b < P; ++b) {
+        if (b % W >= 1) f(b - 1, b, 0);
+        if (b + W < P) f(b + W, b, 1);
+    }
+}
+
+// CColorWeight edges (integer weights) in edge::operator< order (SegmentTree.h:103-111): a counting sort
+// by weight filled in (b, a) order is that order exactly.
+std::vector<Edge> sorted_edges_u8(const uint8_t* wr, const uint8_t* wu, int W, int P) {
     std::vector<int> cnt(257, 0);
-    auto each_edge = [&](auto&& f) {
-        for (int b = 0; b < P; ++b) {
-            const int x = b % W;
-            if (x >= 1) f(b - 1, b, wr[b - 1]);           // (b-1, b): right neighbour of b-1
-            if (b + W < P) f(b + W, b, wu[b + W]);        // (b+W, b): upper neighbour of b+W
-        }
-    };
-    each_edge([&](int, int, uint8_t w) { cnt[w + 1]++; });
+    each_edge(W, P, [&](int a, int, int up) { cnt[(up ? wu[a] : wr[a]) + 1]++; });
     for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
-    const int nE = cnt[256];
-    std::vector<E> e(nE);
-    each_edge([&](int a, int b, uint8_t w) { e[cnt[w]++] = E{a, b, (float)w}; });
+    std::vector<Edge> e(cnt[256]);
+    each_edge(W, P, [&](int a, int b, int up) {
+        const uint8_t w = up ? wu[a] : wr[a];
+        e[cnt[w]++] = Edge{a, b, (float)w};
+    });
+    return e;
+}
+
+// Float-weighted edges (CColorDepthWeight) in edge::operator< order: generated in (b, a) order, then a
+// stable LSD radix sort on the weights' bit patterns (non-negative floats order as their bits).
+std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P) {
+    std::vector<Edge> e, tmp;
+    e.reserve((size_t)2 * P);
+    each_edge(W, P, [&](int a, int b, int up) { e.push_back(Edge{a, b, up ? wu[a] : wr[a]}); });
+    tmp.resize(e.size());
+    for (int shift = 0; shift < 32; shift += 8) {
+        size_t cnt[257] = {0};
+        for (const Edge& x : e) cnt[((__builtin_bit_cast(uint32_t, x.w) >> shift) & 0xFFu) + 1]++;
+        if (cnt[1] == e.size() && shift > 0) continue;   // every key has a zero digit here
+        for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
+        for (const Edge& x : e) tmp[cnt[(__builtin_bit_cast(uint32_t, x.w) >> shift) & 0xFFu]++] = x;
+        e.swap(tmp);
+    }
+    return e;
+}
+
+// BuildSegmentTree (SegmentTree.cpp:38-139) from sorted edges (consumed): segment_graph, the neighbour
+// lists with dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255 colour + depth),
+// BFS from pixel 0, level by level.
+bool tree_from_edges(std::vector<Edge>& e, int P, float tau, float wscale, HostTree& t) {
+#pragma clang fp contract(off)
+    const int nE = (int)e.size();
     // segment_graph (segment-graph.h:48-101)
     Dsu u(P);
     std::vector<float> thr(P, tau / 1);
@@ -264,17 +335,25 @@ bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, H
             if (size_min > 50) e[i].w += 5;   // MIN_SIZE_SEG, PENALTY_CROSS_SEG
         }
     }
-    // neighbour lists in sorted-edge order, dist = min(int(w * 1 + 0.5), 255) (SegmentTree.cpp:74-95)
-    std::vector<int> adj((size_t)P * 4);
-    std::vector<uint8_t> adjd((size_t)P * 4), na(P, 0);
+    // neighbour lists in sorted-edge order (SegmentTree.cpp:74-95), one 24-B record per pixel
+    struct Adj {
+        int q[4];
+        uint8_t d[4];
+        int n;
+    };
+    std::vector<Adj> adj(P);
+    for (int p = 0; p < P; ++p) adj[p].n = 0;
     for (int i = 0; i < nE; ++i) {
         if (!mask[i]) continue;
         const int pa = e[i].a, pb = e[i].b;
-        const uint8_t dis = (uint8_t)std::min((int)(e[i].w * 1.0f + 0.5f), 255);
-        adj[(size_t)pa * 4 + na[pa]] = pb;
-        adjd[(size_t)pa * 4 + na[pa]++] = dis;
-        adj[(size_t)pb * 4 + na[pb]] = pa;
-        adjd[(size_t)pb * 4 + na[pb]++] = dis;
+        const float sw = e[i].w * wscale;
+        const uint8_t dis = (uint8_t)std::min((int)(sw + 0.5f), 255);
+        Adj& A = adj[pa];
+        A.q[A.n] = pb;
+        A.d[A.n++] = dis;
+        Adj& B = adj[pb];
+        B.q[B.n] = pa;
+        B.d[B.n++] = dis;
     }
     // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level
     t.node.assign(P, 0);
@@ -294,11 +373,12 @@ bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, H
             t.rank[p] = i;
             t.first[i] = end;
             uint32_t ch = 0, n = 0;
-            for (int k = 0; k < na[p]; ++k) {
-                const int q = adj[(size_t)p * 4 + k];
+            const Adj& A = adj[p];
+            for (int k = 0; k < A.n; ++k) {
+                const int q = A.q[k];
                 if (vis[q]) continue;
                 vis[q] = 1;
-                const uint8_t dis = adjd[(size_t)p * 4 + k];
+                const uint8_t dis = A.d[k];
                 ch |= (uint32_t)dis << (8 * (n + 1));
                 ++n;
                 t.node[end] = q;
@@ -312,6 +392,31 @@ bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, H
     return end == P;
 }
 
+bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
+    std::vector<Edge> e = sorted_edges_u8(wr, wu, W, W * H);
+    return tree_from_edges(e, W * H, tau, 1.0f, t);
+}
+
+// CColorDepthWeight::GetWeight (SegmentTree.cpp:204-219) from the colour weights (max channel |diff| on
+// the 3x3-median guide), the first left map and the mask, in the reference's float operations
+void depth_weights(const uint8_t* wr, const uint8_t* wu, const uint8_t* disp, const uint8_t* mask, int W, int H,
+                   float level, float* fr, float* fu) {
+#pragma clang fp contract(off)
+    auto weight = [&](int p, int q, uint8_t c) -> float {
+        if (mask[p] && mask[q]) {
+            const float dispValue = (float)std::abs(disp[p] - disp[q]) / level;
+            const float colorValue = (float)c / 255.0f;
+            return 0.5f * dispValue + (1.0f - 0.5f) * colorValue;
+        }
+        return (float)c / 255.0f;
+    };
+    const int P = W * H;
+    for (int p = 0; p < P; ++p) {
+        fr[p] = (p % W + 1 < W) ? weight(p, p + 1, wr[p]) : 0.f;
+        fu[p] = (p >= W) ? weight(p, p - W, wu[p]) : 0.f;
+    }
+}
+
 template <class T>
 hipError_t grow(T*& p, size_t& have, size_t n) {
     if (have >= n) return hipSuccess;
@@ -321,6 +426,59 @@ hipError_t grow(T*& p, size_t& have, size_t n) {
     hipError_t e = hipMalloc(&p, n * sizeof(T));
     if (e == hipSuccess) have = n;
     return e;
+}
+
+// One tree on the device: workspace slot k holds int [rank | parent | first | child | lev] (5P + 2),
+// uint8 pdist (P) and the 256-entry weight table.
+struct DevTree {
+    int* rank;
+    int* parent;
+    int* first;
+    uint32_t* child;
+    int* lev;
+    uint8_t* pdist;
+    float* table;
+    int nlev;
+};
+
+DevTree tree_slot(StWorkspace& ws, int64_t P, int k) {
+    DevTree d{};
+    d.rank = ws.tree_i + (size_t)k * (5 * P + 2);
+    d.parent = d.rank + P;
+    d.first = d.parent + P;
+    d.child = reinterpret_cast<uint32_t*>(d.first + P);
+    d.lev = reinterpret_cast<int*>(d.child + P);
+    d.pdist = ws.tree_b + (size_t)k * P;
+    d.table = ws.table + (size_t)k * 256;
+    return d;
+}
+
+// UpdateTable (SegmentTree.cpp:141-146)
+void weight_table(float sigma, float* table) {
+    const float sg = std::max(0.01f, sigma);
+    for (int i = 0; i <= 255; ++i) table[i] = std::exp(-float(i) / (255 * sg));
+}
+
+// `t` and `table` must stay alive until the stream has consumed the copies
+hipError_t upload_tree(const HostTree& t, const float* table, int64_t P, DevTree& d, hipStream_t s) {
+    d.nlev = (int)t.lev.size() - 1;
+    if ((size_t)d.nlev + 1 > (size_t)P + 2) return hipErrorInvalidValue;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(d.rank, t.rank.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.parent, t.parent.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.first, t.first.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.child, t.child.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.lev, t.lev.data(), t.lev.size() * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.pdist, t.pdist.data(), (size_t)P, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    return hipMemcpyAsync(d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s);
+}
+
+FilterJob filter_job(float* C, float* F, const DevTree& d) {
+    return FilterJob{C, F, d.parent, d.pdist, d.first, d.child, d.lev, d.nlev, d.table};
+}
+
+float ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace
@@ -343,17 +501,17 @@ void StWorkspace::release() {
     w8_n = grad_n = vol_n = tree_i_n = tree_b_n = table_n = 0;
 }
 
+#define ST_CHK(x)                          \
+    do {                                   \
+        const hipError_t e_ = (x);         \
+        if (e_ != hipSuccess) return e_;   \
+    } while (0)
+
 hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch, int D,
                               int scale, float sigma, float tau, uint8_t* d_out, hipStream_t s, StStats* st) {
     if (W < 2 || H < 1 || D < 1 || D > kMaxDisp || scale < 0) return hipErrorInvalidValue;
     const int64_t P = (int64_t)W * H;
     if (P > (1 << 28)) return hipErrorInvalidValue;
-    hipError_t e;
-#define ST_CHK(x)          \
-    do {                   \
-        e = (x);           \
-        if (e != hipSuccess) return e; \
-    } while (0)
     ST_CHK(grow(ws.w8, ws.w8_n, (size_t)P * 3));
     ST_CHK(grow(ws.grad, ws.grad_n, (size_t)P * 2));
     ST_CHK(grow(ws.vol, ws.vol_n, (size_t)P * D * 2));
@@ -377,44 +535,132 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     const auto t0 = std::chrono::steady_clock::now();
     HostTree t;
     if (!build_tree(hw.data(), hw.data() + P, W, H, tau, t)) return hipErrorInvalidValue;
-    const int nlev = (int)t.lev.size() - 1;
-    if ((size_t)nlev + 1 > (size_t)P + 2) return hipErrorInvalidValue;
     float table[256];
-    const float sg = std::max(0.01f, sigma);
-    for (int i = 0; i <= 255; ++i) table[i] = std::exp(-float(i) / (255 * sg));   // UpdateTable, :141-146
-    const auto t1 = std::chrono::steady_clock::now();
-    // tree arrays: int [rank | parent | first | child | lev], uint8 pdist
-    int* d_rank = ws.tree_i;
-    int* d_parent = d_rank + P;
-    int* d_first = d_parent + P;
-    uint32_t* d_child = reinterpret_cast<uint32_t*>(d_first + P);
-    int* d_lev = reinterpret_cast<int*>(d_child + P);
-    ST_CHK(hipMemcpyAsync(d_rank, t.rank.data(), (size_t)P * 4, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(d_parent, t.parent.data(), (size_t)P * 4, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(d_first, t.first.data(), (size_t)P * 4, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(d_child, t.child.data(), (size_t)P * 4, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(d_lev, t.lev.data(), t.lev.size() * 4, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(ws.tree_b, t.pdist.data(), (size_t)P, hipMemcpyHostToDevice, s));
-    ST_CHK(hipMemcpyAsync(ws.table, table, sizeof(table), hipMemcpyHostToDevice, s));
+    weight_table(sigma, table);
+    const float tree_ms = ms_since(t0);
+    DevTree dt = tree_slot(ws, P, 0);
+    ST_CHK(upload_tree(t, table, P, dt, s));
     float* C = ws.vol;
     float* F = ws.vol + (size_t)P * D;
-    hipLaunchKernelGGL(st_cost_kernel, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P, d_rank, D, C);
+    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
+                       dt.rank, D, C);
     ST_CHK(hipGetLastError());
-    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D), dim3(1024), 0, s, C, F, d_parent, ws.tree_b, d_first,
-                       d_child, d_lev, nlev, (int)P, ws.table);
+    FilterJobs jobs{};
+    jobs.j[0] = filter_job(C, F, dt);
+    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 1), dim3(kFT), 0, s, jobs, (int)P);
     ST_CHK(hipGetLastError());
     uint8_t* raw = ws.w8;   // the weights are consumed: reuse for the unfiltered map
-    hipLaunchKernelGGL(st_wta_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, F, d_rank, (int)P, D,
+    hipLaunchKernelGGL(st_wta_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, F, dt.rank, (int)P, D,
                        scale, raw);
     ST_CHK(hipGetLastError());
     ST_CHK(launch_median(raw, W, H, W, P, 1, 3, d_out, W, P, s));   // MeanFilter(disparity, disparity, 3)
     if (st) {
-        st->levels = nlev;
-        st->tree_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+        st->levels = dt.nlev;
+        st->tree_ms = tree_ms;
     }
-#undef ST_CHK
     // keep the host tree alive until its uploads have been consumed
     return hipStreamSynchronize(s);
 }
+
+hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch,
+                                      int D, int scale, float sigma, float tau, uint8_t* d_out, hipStream_t s,
+                                      StStats* st) {
+    if (W < 2 || H < 1 || D < 1 || D > kMaxDisp || scale < 0) return hipErrorInvalidValue;
+    const int64_t P = (int64_t)W * H;
+    if (P > (1 << 28)) return hipErrorInvalidValue;
+    constexpr float kSigmaOne = 0.08f;   // SIGMA_ONE, Toolkit.h:35
+    ST_CHK(grow(ws.w8, ws.w8_n, (size_t)P * 10));
+    ST_CHK(grow(ws.grad, ws.grad_n, (size_t)P * 2));
+    ST_CHK(grow(ws.vol, ws.vol_n, (size_t)P * D * 4));
+    ST_CHK(grow(ws.tree_i, ws.tree_i_n, ((size_t)P * 5 + 2) * 2));
+    ST_CHK(grow(ws.tree_b, ws.tree_b_n, (size_t)P * 2));
+    ST_CHK(grow(ws.table, ws.table_n, (size_t)512));
+    const dim3 rows((unsigned)((W + kST - 1) / kST), (unsigned)H);
+    const dim3 pix((unsigned)((P + kST - 1) / kST));
+    uint8_t* wrL = ws.w8;
+    uint8_t* wrR = ws.w8 + 2 * P;
+    uint8_t* raw0 = ws.w8 + 4 * P;
+    uint8_t* raw1 = ws.w8 + 5 * P;
+    uint8_t* mapL = ws.w8 + 6 * P;   // first-pass maps after the 7x7 median
+    uint8_t* mapR = ws.w8 + 7 * P;
+    uint8_t* chk = ws.w8 + 8 * P;
+    uint8_t* mask = ws.w8 + 9 * P;
+    // colour weights of both views (wr, wu planes each) -> host; gradients
+    hipLaunchKernelGGL(st_weights_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, wrL, wrL + P);
+    hipLaunchKernelGGL(st_weights_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, wrR, wrR + P);
+    ST_CHK(hipGetLastError());
+    std::vector<uint8_t> hw((size_t)P * 4);
+    ST_CHK(hipMemcpyAsync(hw.data(), ws.w8, (size_t)P * 4, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
+    hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
+    ST_CHK(hipGetLastError());
+    ST_CHK(hipStreamSynchronize(s));
+    // first run: colour trees of the left and the right view, built side by side (StereoDisparity.cpp:112-123)
+    auto t0 = std::chrono::steady_clock::now();
+    HostTree tl, tr;
+    bool okR = false;
+    std::thread th([&] { okR = build_tree(hw.data() + 2 * P, hw.data() + 3 * P, W, H, tau, tr); });
+    const bool okL = build_tree(hw.data(), hw.data() + P, W, H, tau, tl);
+    th.join();
+    if (!okL || !okR) return hipErrorInvalidValue;
+    float tab1[256];
+    weight_table(kSigmaOne, tab1);
+    float tree_ms = ms_since(t0);
+    DevTree d0 = tree_slot(ws, P, 0), d1 = tree_slot(ws, P, 1);
+    ST_CHK(upload_tree(tl, tab1, P, d0, s));
+    ST_CHK(upload_tree(tr, tab1, P, d1, s));
+    float* C0 = ws.vol;
+    float* F0 = ws.vol + (size_t)P * D;
+    float* C1 = ws.vol + (size_t)P * D * 2;
+    float* F1 = ws.vol + (size_t)P * D * 3;
+    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
+                       d0.rank, D, C0);
+    hipLaunchKernelGGL(st_cost_kernel<true>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
+                       d1.rank, D, C1);
+    ST_CHK(hipGetLastError());
+    FilterJobs jobs{};
+    jobs.j[0] = filter_job(C0, F0, d0);
+    jobs.j[1] = filter_job(C1, F1, d1);
+    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 2), dim3(kFT), 0, s, jobs, (int)P);
+    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, 1, raw0);
+    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F1, d1.rank, (int)P, D, 1, raw1);
+    ST_CHK(hipGetLastError());
+    ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, mapL, W, P, s));   // MeanFilter(disparityLeft, ..., 3)
+    ST_CHK(launch_median(raw1, W, H, W, P, 1, 3, mapR, W, P, s));
+    // left-right check (StereoDisparity.cpp:129-147): mask = !occluded
+    ST_CHK(launch_lr_check(mapL, W, P, mapR, W, P, 0, W, H, 1, chk, W, P, nullptr, mask, W, P, s));
+    std::vector<uint8_t> hmap((size_t)P), hmask((size_t)P);
+    ST_CHK(hipMemcpyAsync(hmap.data(), mapL, (size_t)P, hipMemcpyDeviceToHost, s));
+    ST_CHK(hipMemcpyAsync(hmask.data(), mask, (size_t)P, hipMemcpyDeviceToHost, s));
+    ST_CHK(hipStreamSynchronize(s));
+    // re-segmentation: colour + depth tree on the left view (StereoDisparity.cpp:150-152)
+    t0 = std::chrono::steady_clock::now();
+    std::vector<float> fw((size_t)P * 2);
+    depth_weights(hw.data(), hw.data() + P, hmap.data(), hmask.data(), W, H, (float)D, fw.data(), fw.data() + P);
+    std::vector<Edge> e = sorted_edges_f(fw.data(), fw.data() + P, W, (int)P);
+    HostTree td;
+    if (!tree_from_edges(e, (int)P, tau, 255.0f, td)) return hipErrorInvalidValue;
+    float tab2[256];
+    weight_table(sigma, tab2);
+    tree_ms += ms_since(t0);
+    ST_CHK(upload_tree(td, tab2, P, d0, s));
+    // second run on the same cost (the reference recomputes it, :150)
+    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
+                       d0.rank, D, C0);
+    ST_CHK(hipGetLastError());
+    FilterJobs job2{};
+    job2.j[0] = filter_job(C0, F0, d0);
+    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 1), dim3(kFT), 0, s, job2, (int)P);
+    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, scale, raw0);
+    ST_CHK(hipGetLastError());
+    ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, d_out, W, P, s));
+    if (st) {
+        st->levels = d0.nlev;
+        st->tree_ms = tree_ms;
+    }
+    return hipStreamSynchronize(s);
+}
+
+#undef ST_CHK
 
 }  // namespace sm

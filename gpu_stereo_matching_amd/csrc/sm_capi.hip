@@ -1053,9 +1053,11 @@ SM_API int sm_median_u8_device(sm_handle* h, const uint8_t* d_src, int width, in
     return SM_OK;
 }
 
-SM_API int sm_segment_tree_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
-                                        int height, int pitch, int max_level, int scale, float sigma,
-                                        uint8_t* disp_out, int out_pitch) {
+namespace {
+// segment-tree stereo behind both C entry points: refined = false ST-1, true ST-2
+int segment_tree_call(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width, int height,
+                      int pitch, int max_level, int scale, float sigma, uint8_t* disp_out, int out_pitch,
+                      bool refined) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
     if (!left_bgr || !right_bgr || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
     if (width < 2 || height < 1 || pitch < 3 * width || out_pitch < width)
@@ -1084,13 +1086,33 @@ SM_API int sm_segment_tree_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, c
     SM_HIP(copy2d(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
     SM_HIP(copy2d(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
     h->st_valid = false;
-    SM_HIP(sm::segment_tree_match(h->st, dl, dr, width, height, (int)row, max_level, scale, sigma, 1200.0f, h->d_disp, s,
-                                  &h->st_stats));
+    constexpr float kTau = 1200.0f;   // TAU, Toolkit.h:34
+    if (refined)
+        SM_HIP(sm::segment_tree_refined_match(h->st, dl, dr, width, height, (int)row, max_level, scale, sigma, kTau,
+                                              h->d_disp, s, &h->st_stats));
+    else
+        SM_HIP(sm::segment_tree_match(h->st, dl, dr, width, height, (int)row, max_level, scale, sigma, kTau, h->d_disp,
+                                      s, &h->st_stats));
     SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
     h->st_total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     h->st_valid = true;
     return SM_OK;
+}
+}  // namespace
+
+SM_API int sm_segment_tree_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
+                                        int height, int pitch, int max_level, int scale, float sigma,
+                                        uint8_t* disp_out, int out_pitch) {
+    return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
+                             out_pitch, false);
+}
+
+SM_API int sm_segment_tree_refined_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
+                                          int height, int pitch, int max_level, int scale, float sigma,
+                                          uint8_t* disp_out, int out_pitch) {
+    return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
+                             out_pitch, true);
 }
 
 SM_API int sm_last_segment_tree_stats(sm_handle* h, float* tree_ms, float* total_ms, int* levels) {

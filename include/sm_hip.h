@@ -222,7 +222,18 @@ SM_API int sm_block_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const ui
 SM_API int sm_segment_tree_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,
                                         int width, int height, int pitch, int max_level, int scale, float sigma,
                                         uint8_t *disp_out, int out_pitch);
-/* last segment-tree call: host tree-build time, whole-call time (ms) and the tree's BFS level count */
+/* STMatching's ST-2 (stereo_disparity_iteration, StereoDisparity.cpp:91-160; main.cpp's method 1), same
+ * arguments and output as sm_segment_tree_match_bgr_u8: first-pass left and right maps on colour trees
+ * of each view (sigma SIGMA_ONE = 0.08, Toolkit.h:35; the right cost taken from the left's,
+ * StereoHelper.cpp:156-180), each WTA + 7x7 median; the left-right check (:129-147); then a colour +
+ * depth tree (CColorDepthWeight, SegmentTree.cpp:196-219) on the left view, the first left map and
+ * the check's mask, filtered with `sigma`, WTA, 7x7 median, x scale.  The three trees are built on the
+ * host (the first two on two threads); everything O(P*D) runs on the GPU.  Synchronous. */
+SM_API int sm_segment_tree_refined_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,
+                                          int width, int height, int pitch, int max_level, int scale, float sigma,
+                                          uint8_t *disp_out, int out_pitch);
+/* last segment-tree call (either method): host tree-build time, whole-call time (ms) and the last tree's
+ * BFS level count */
 SM_API int sm_last_segment_tree_stats(sm_handle *h, float *tree_ms, float *total_ms, int *levels);
 
 /* ---- several GPUs from one host thread (sm_create_group) ----

@@ -73,6 +73,14 @@ def lib():
         L.ora_st_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                   ctypes.c_float, _u8p]
         L.ora_st_disp.restype = ctypes.c_int
+        _fp = ctypes.POINTER(ctypes.c_float)
+        L.ora_st_right_cost.argtypes = [_fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp]
+        L.ora_st_tree_depth.argtypes = [_u8p, _u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                        _i32p, _i32p, _u8p, _i32p, _u8p, _u8p]
+        L.ora_st_tree_depth.restype = ctypes.c_int
+        L.ora_st2_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_float, _u8p, _u8p, _u8p, _u8p]
+        L.ora_st2_disp.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -304,6 +312,41 @@ def st_disp(left_bgr, right_bgr, D: int = 60, scale: int = 4, sigma: float = 0.1
     out = np.empty((H, W), np.uint8)
     levels = lib().ora_st_disp(_p(L, _u8p), _p(R, _u8p), W, H, D, scale, sigma, tau, _p(out, _u8p))
     return out, levels
+
+
+def st_right_cost(cost) -> np.ndarray:
+    """STMatching GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180) of a float [H, W, D] volume."""
+    c = np.ascontiguousarray(cost, dtype=np.float32)
+    H, W, D = c.shape
+    out = np.empty_like(c)
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib().ora_st_right_cost(c.ctypes.data_as(fp), W, H, D, out.ctypes.data_as(fp))
+    return out
+
+
+def st_tree_depth(left_bgr, disp, mask, level: int, tau: float = 1200.0):
+    """BuildSegmentTree with CColorDepthWeight (SegmentTree.cpp:196-219): same dict as st_tree."""
+    L = _bgr(left_bgr)
+    H, W = L.shape[:2]
+    P = W * H
+    d, m = _img(disp), _img(mask)
+    t = dict(node=np.empty(P, np.int32), parent=np.empty(P, np.int32), pdist=np.empty(P, np.uint8),
+             first=np.empty(P, np.int32), nchild=np.empty(P, np.uint8), cdist=np.zeros((P, 4), np.uint8))
+    t["levels"] = lib().ora_st_tree_depth(_p(L, _u8p), _p(d, _u8p), _p(m, _u8p), W, H, level, tau,
+                                          _p(t["node"], _i32p), _p(t["parent"], _i32p), _p(t["pdist"], _u8p),
+                                          _p(t["first"], _i32p), _p(t["nchild"], _u8p), _p(t["cdist"], _u8p))
+    return t
+
+
+def st2_disp(left_bgr, right_bgr, D: int = 60, scale: int = 4, sigma: float = 0.1, tau: float = 1200.0):
+    """STMatching stereo_disparity_iteration (ST-2, StereoDisparity.cpp:91-160).
+    Returns (disp, levels, first-pass left map, first-pass right map, LR mask)."""
+    L, R = _bgr(left_bgr), _bgr(right_bgr)
+    H, W = L.shape[:2]
+    out, l1, r1, mk = (np.empty((H, W), np.uint8) for _ in range(4))
+    levels = lib().ora_st2_disp(_p(L, _u8p), _p(R, _u8p), W, H, D, scale, sigma, tau, _p(out, _u8p), _p(l1, _u8p),
+                                _p(r1, _u8p), _p(mk, _u8p))
+    return out, levels, l1, r1, mk
 
 
 def synth_pair(seed: int, W: int, H: int, D: int):

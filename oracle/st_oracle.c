@@ -8,6 +8,8 @@
  * binary is therefore unpinned; the float operations are written in the reference's
  * order (no FMA contraction: the Makefile passes -ffp-contract=off).
  *
+ * ST-2 ("ST_REFINED", StereoDisparity.cpp:91-160) reuses these pieces: ora_st2_disp below.
+ *
  * Pipeline (ST_RAW):
  *   1. cost volume  C[y][x][d]: truncated colour + gradient cost   (StereoHelper.cpp:37-129)
  *   2. guide        3x3 median of the left BGR image (ctmf, r = 1)  (SegmentTree.cpp:183-194, Toolkit.cpp:33-48)
@@ -110,25 +112,39 @@ static int st_edge_cmp(const void *pa, const void *pb)
     return (x->a > y->a) - (x->a < y->a);
 }
 
-/* BuildSegmentTree (SegmentTree.cpp:38-139) with CColorWeight (:183-194): the tree in BFS order from
- * pixel 0.  Outputs per BFS position i: node[i] (pixel id), parent[i] (BFS position, -1 at the root),
- * pdist[i] (edge distance to the parent), first[i] / nchild[i] (children occupy BFS positions
- * first .. first + nchild - 1) and cdist[4 * i + k].  Returns the number of BFS levels. */
-ORA_API int ora_st_tree(const uint8_t *Lbgr, int W, int H, float tau, int *node, int *parent, uint8_t *pdist,
-                        int *first, uint8_t *nchild, uint8_t *cdist)
+/* MeanFilter(img, img, 1) of a BGR image: ctmf r = 1 per channel (SegmentTree.cpp:185, :199) */
+static uint8_t *st_guide(const uint8_t *bgr, int W, int H)
 {
     const int P = W * H;
-    /* guide: MeanFilter(img, img, 1) = ctmf r = 1 per channel (SegmentTree.cpp:185) */
     uint8_t *ch = (uint8_t *)malloc((size_t)P), *med = (uint8_t *)malloc((size_t)P * 3), *tmp = (uint8_t *)malloc((size_t)P);
     for (int c = 0; c < 3; ++c) {
-        for (int p = 0; p < P; ++p) ch[p] = Lbgr[(size_t)p * 3 + c];
+        for (int p = 0; p < P; ++p) ch[p] = bgr[(size_t)p * 3 + c];
         ora_median_u8(ch, W, H, 1, tmp);
         for (int p = 0; p < P; ++p) med[(size_t)p * 3 + c] = tmp[p];
     }
     free(ch);
     free(tmp);
-    /* edges, SegmentTree.cpp:44-62: right neighbour, then the one above; weight = max channel |diff| */
-    st_edge *edges = (st_edge *)malloc(sizeof(st_edge) * (size_t)P * 2);
+    return med;
+}
+
+/* max channel |diff| of two guide pixels (CColorWeight::GetWeight, SegmentTree.cpp:189-194) */
+static int st_color_diff(const uint8_t *med, int p, int q)
+{
+    int m = 0;
+    for (int c = 0; c < 3; ++c) {
+        const int v = abs(med[(size_t)p * 3 + c] - med[(size_t)q * 3 + c]);
+        m = v > m ? v : m;
+    }
+    return m;
+}
+
+/* edges of SegmentTree.cpp:44-62 (right neighbour, then the one above).  disp == NULL: CColorWeight
+ * (weight = max channel |diff|, :189-194); else CColorDepthWeight (:196-219): where both ends are in
+ * `mask`, 0.5 * |disp diff| / level + 0.5 * colour / 255, else colour / 255 */
+static st_edge *st_edges(const uint8_t *med, int W, int H, const uint8_t *disp, const uint8_t *mask, float level,
+                         int *nE)
+{
+    st_edge *edges = (st_edge *)malloc(sizeof(st_edge) * (size_t)W * H * 2);
     int E = 0;
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
@@ -142,18 +158,36 @@ ORA_API int ora_st_tree(const uint8_t *Lbgr, int W, int H, float tau, int *node,
                     if (y < 1) continue;
                     q = p - W;
                 }
-                int m = 0;
-                for (int c = 0; c < 3; ++c) {
-                    const int v = abs(med[(size_t)p * 3 + c] - med[(size_t)q * 3 + c]);
-                    m = v > m ? v : m;
+                const int m = st_color_diff(med, p, q);
+                float w;
+                if (!disp) {
+                    w = (float)m;
+                } else if (mask[p] && mask[q]) {
+                    const float dispValue = (float)abs(disp[p] - disp[q]) / level;
+                    const float colorValue = (float)m / 255.0f;
+                    w = 0.5f * dispValue + (1.0f - 0.5f) * colorValue;
+                } else {
+                    w = (float)m / 255.0f;
                 }
                 edges[E].a = p;
                 edges[E].b = q;
-                edges[E].w = (float)m;
+                edges[E].w = w;
                 ++E;
             }
         }
-    free(med);
+    *nE = E;
+    return edges;
+}
+
+/* BuildSegmentTree (SegmentTree.cpp:38-139) from its edge list (consumed): segment_graph, the
+ * node-based graph with dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 for
+ * CColorWeight, 255 for CColorDepthWeight), BFS from pixel 0.  Outputs per BFS position i: node[i]
+ * (pixel id), parent[i] (BFS position, -1 at the root), pdist[i] (edge distance to the parent),
+ * first[i] / nchild[i] (children occupy BFS positions first .. first + nchild - 1) and cdist[4 * i + k].
+ * Returns the number of BFS levels (-1 if the tree does not span the image). */
+static int st_tree_from_edges(st_edge *edges, int E, int P, float tau, float wscale, int *node, int *parent,
+                              uint8_t *pdist, int *first, uint8_t *nchild, uint8_t *cdist)
+{
     /* segment_graph, segment-graph.h:48-101 */
     qsort(edges, (size_t)E, sizeof(st_edge), st_edge_cmp);
     st_elt *u = (st_elt *)malloc(sizeof(st_elt) * (size_t)P);
@@ -181,13 +215,13 @@ ORA_API int ora_st_tree(const uint8_t *Lbgr, int W, int H, float tau, int *node,
     }
     free(thr);
     free(u);
-    /* node-based graph, SegmentTree.cpp:71-95: neighbours in sorted-edge order, dist = min(int(w + 0.5), 255) */
+    /* node-based graph, SegmentTree.cpp:71-95: neighbours in sorted-edge order */
     int *adj = (int *)malloc(sizeof(int) * (size_t)P * 4);
     uint8_t *adjd = (uint8_t *)malloc((size_t)P * 4), *na = (uint8_t *)calloc((size_t)P, 1);
     for (int i = 0; i < E; ++i) {
         if (!mask[i]) continue;
         const int pa = edges[i].a, pb = edges[i].b;
-        int dis = (int)(edges[i].w * 1.0f + 0.5f);
+        int dis = (int)(edges[i].w * wscale + 0.5f);
         dis = dis < 255 ? dis : 255;
         adj[pa * 4 + na[pa]] = pb;
         adjd[pa * 4 + na[pa]++] = (uint8_t)dis;
@@ -195,7 +229,6 @@ ORA_API int ora_st_tree(const uint8_t *Lbgr, int W, int H, float tau, int *node,
         adjd[pb * 4 + na[pb]++] = (uint8_t)dis;
     }
     free(mask);
-    free(edges);
     /* BFS from pixel 0, SegmentTree.cpp:97-130 */
     uint8_t *vis = (uint8_t *)calloc((size_t)P, 1);
     int *level = (int *)malloc(sizeof(int) * (size_t)P);
@@ -231,6 +264,33 @@ ORA_API int ora_st_tree(const uint8_t *Lbgr, int W, int H, float tau, int *node,
     return end == P ? levels : -1;
 }
 
+/* BuildSegmentTree with CColorWeight on `bgr` (SegmentTree.cpp:38-139, :183-194) */
+ORA_API int ora_st_tree(const uint8_t *bgr, int W, int H, float tau, int *node, int *parent, uint8_t *pdist,
+                        int *first, uint8_t *nchild, uint8_t *cdist)
+{
+    uint8_t *med = st_guide(bgr, W, H);
+    int E;
+    st_edge *edges = st_edges(med, W, H, NULL, NULL, 0.f, &E);
+    free(med);
+    const int levels = st_tree_from_edges(edges, E, W * H, tau, 1.0f, node, parent, pdist, first, nchild, cdist);
+    free(edges);
+    return levels;
+}
+
+/* BuildSegmentTree with CColorDepthWeight(img, disp, mask, maxLevel) (SegmentTree.cpp:196-219, scale 255) */
+ORA_API int ora_st_tree_depth(const uint8_t *bgr, const uint8_t *disp, const uint8_t *mask, int W, int H, int level,
+                              float tau, int *node, int *parent, uint8_t *pdist, int *first, uint8_t *nchild,
+                              uint8_t *cdist)
+{
+    uint8_t *med = st_guide(bgr, W, H);
+    int E;
+    st_edge *edges = st_edges(med, W, H, disp, mask, (float)level, &E);
+    free(med);
+    const int levels = st_tree_from_edges(edges, E, W * H, tau, 255.0f, node, parent, pdist, first, nchild, cdist);
+    free(edges);
+    return levels;
+}
+
 /* Filter, SegmentTree.cpp:141-181, on the pixel-major volume cost[p * D + d] (in place) */
 ORA_API void ora_st_filter(const int *node, const int *parent, const uint8_t *pdist, const int *first,
                            const uint8_t *nchild, const uint8_t *cdist, int P, int D, float sigma, float *cost)
@@ -258,22 +318,34 @@ ORA_API void ora_st_filter(const int *node, const int *parent, const uint8_t *pd
     free(buf);
 }
 
-/* stereo_disparity_normal (StereoDisparity.cpp:57-89): cost, tree on the left view, filter, float WTA
- * (strict < from d = 0, StereoHelper.cpp:131-154), 7x7 median (MeanFilter r = 3), x scale (saturated).
- * Returns the tree's BFS level count (-1 if the tree does not span the image). */
-ORA_API int ora_st_disp(const uint8_t *Lbgr, const uint8_t *Rbgr, int W, int H, int D, int scale, float sigma,
-                        float tau, uint8_t *out)
+typedef struct {
+    int *node, *parent, *first;
+    uint8_t *pdist, *nchild, *cdist;
+} st_tree_buf;
+
+static void st_tree_alloc(st_tree_buf *t, int P)
 {
-    const int P = W * H;
-    float *cost = (float *)malloc(sizeof(float) * (size_t)P * D);
-    ora_st_cost(Lbgr, Rbgr, W, H, D, cost);
-    int *node = (int *)malloc(sizeof(int) * (size_t)P), *parent = (int *)malloc(sizeof(int) * (size_t)P);
-    int *first = (int *)malloc(sizeof(int) * (size_t)P);
-    uint8_t *pdist = (uint8_t *)malloc((size_t)P), *nchild = (uint8_t *)malloc((size_t)P);
-    uint8_t *cdist = (uint8_t *)calloc((size_t)P * 4, 1);
-    const int levels = ora_st_tree(Lbgr, W, H, tau, node, parent, pdist, first, nchild, cdist);
-    if (levels > 0) ora_st_filter(node, parent, pdist, first, nchild, cdist, P, D, sigma, cost);
-    uint8_t *disp = (uint8_t *)malloc((size_t)P);
+    t->node = (int *)malloc(sizeof(int) * (size_t)P);
+    t->parent = (int *)malloc(sizeof(int) * (size_t)P);
+    t->first = (int *)malloc(sizeof(int) * (size_t)P);
+    t->pdist = (uint8_t *)malloc((size_t)P);
+    t->nchild = (uint8_t *)malloc((size_t)P);
+    t->cdist = (uint8_t *)calloc((size_t)P * 4, 1);
+}
+
+static void st_tree_free(st_tree_buf *t)
+{
+    free(t->node);
+    free(t->parent);
+    free(t->first);
+    free(t->pdist);
+    free(t->nchild);
+    free(t->cdist);
+}
+
+/* GetDisparity_WTA (StereoHelper.cpp:131-154): strict < from d = 0, pixel-major cost */
+static void st_wta(const float *cost, int P, int D, uint8_t *disp)
+{
     for (int p = 0; p < P; ++p) {
         const float *c = cost + (size_t)p * D;
         int m = 0;
@@ -285,18 +357,120 @@ ORA_API int ora_st_disp(const uint8_t *Lbgr, const uint8_t *Rbgr, int W, int H, 
             }
         disp[p] = (uint8_t)m;
     }
+}
+
+/* filter `cost` on `t`, WTA, 7x7 median (MeanFilter r = 3) into out */
+static void st_aggregate(const st_tree_buf *t, int W, int H, int D, float sigma, float *cost, uint8_t *out)
+{
+    const int P = W * H;
+    ora_st_filter(t->node, t->parent, t->pdist, t->first, t->nchild, t->cdist, P, D, sigma, cost);
+    uint8_t *disp = (uint8_t *)malloc((size_t)P);
+    st_wta(cost, P, D, disp);
     ora_median_u8(disp, W, H, 3, out);
-    for (int p = 0; p < P; ++p) {
-        const int v = out[p] * scale;
-        out[p] = (uint8_t)(v > 255 ? 255 : v);
-    }
     free(disp);
+}
+
+static void st_scale(uint8_t *m, int P, int scale)
+{
+    for (int p = 0; p < P; ++p) {
+        const int v = m[p] * scale;
+        m[p] = (uint8_t)(v > 255 ? 255 : v);
+    }
+}
+
+/* stereo_disparity_normal (StereoDisparity.cpp:57-89): cost, tree on the left view, filter, float WTA
+ * (strict < from d = 0, StereoHelper.cpp:131-154), 7x7 median (MeanFilter r = 3), x scale (saturated).
+ * Returns the tree's BFS level count (-1 if the tree does not span the image). */
+ORA_API int ora_st_disp(const uint8_t *Lbgr, const uint8_t *Rbgr, int W, int H, int D, int scale, float sigma,
+                        float tau, uint8_t *out)
+{
+    const int P = W * H;
+    float *cost = (float *)malloc(sizeof(float) * (size_t)P * D);
+    ora_st_cost(Lbgr, Rbgr, W, H, D, cost);
+    st_tree_buf t;
+    st_tree_alloc(&t, P);
+    const int levels = ora_st_tree(Lbgr, W, H, tau, t.node, t.parent, t.pdist, t.first, t.nchild, t.cdist);
+    if (levels > 0) {
+        st_aggregate(&t, W, H, D, sigma, cost, out);
+        st_scale(out, P, scale);
+    }
+    st_tree_free(&t);
     free(cost);
-    free(node);
-    free(parent);
-    free(first);
-    free(pdist);
-    free(nchild);
-    free(cdist);
+    return levels;
+}
+
+/* GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180), pixel-major: the right view's cost at
+ * (y, x, d) is the left view's at (y, x + d, d); where x + d >= W it repeats d - 1's */
+ORA_API void ora_st_right_cost(const float *left, int W, int H, int D, float *right)
+{
+    memcpy(right, left, sizeof(float) * (size_t)W * H * D);
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W - D; ++x)
+            for (int d = 0; d < D; ++d)
+                right[((size_t)y * W + x) * D + d] = left[((size_t)y * W + x + d) * D + d];
+        for (int x = W - D > 0 ? W - D : 0; x < W; ++x)
+            for (int d = 0; d < D; ++d) {
+                if (x + d < W) right[((size_t)y * W + x) * D + d] = left[((size_t)y * W + x + d) * D + d];
+                else right[((size_t)y * W + x) * D + d] = right[((size_t)y * W + x) * D + d - 1];
+            }
+    }
+}
+
+/* stereo_disparity_iteration, ST-2 (StereoDisparity.cpp:91-160):
+ *   left / right maps on CColorWeight trees of each view with sigma = SIGMA_ONE (0.08, Toolkit.h:35), the
+ *   right cost taken from the left's (GetRightMatchingCostFromLeft), each WTA + 7x7 median;
+ *   the left-right check (:129-147): mask = !(x - d < 0 || d == 0 || |d - dR(x - d)| > 1);
+ *   a CColorDepthWeight tree on the left view, the filtered left map and the mask, with `sigma`; its
+ *   WTA + 7x7 median, x scale.
+ * Optional outputs (NULL to skip): the first-pass left / right maps and the mask.  Returns the last
+ * tree's BFS level count (-1 if a tree does not span the image). */
+ORA_API int ora_st2_disp(const uint8_t *Lbgr, const uint8_t *Rbgr, int W, int H, int D, int scale, float sigma,
+                         float tau, uint8_t *out, uint8_t *left1, uint8_t *right1, uint8_t *mask_out)
+{
+    const int P = W * H;
+    const float sigma_one = 0.08f;
+    float *costL = (float *)malloc(sizeof(float) * (size_t)P * D);
+    float *costR = (float *)malloc(sizeof(float) * (size_t)P * D);
+    float *cost2 = (float *)malloc(sizeof(float) * (size_t)P * D);
+    ora_st_cost(Lbgr, Rbgr, W, H, D, costL);
+    ora_st_right_cost(costL, W, H, D, costR);
+    memcpy(cost2, costL, sizeof(float) * (size_t)P * D);   /* the reference recomputes the same volume (:150) */
+    uint8_t *dL = (uint8_t *)malloc((size_t)P), *dR = (uint8_t *)malloc((size_t)P), *mask = (uint8_t *)malloc((size_t)P);
+    st_tree_buf t;
+    st_tree_alloc(&t, P);
+    int levels = ora_st_tree(Lbgr, W, H, tau, t.node, t.parent, t.pdist, t.first, t.nchild, t.cdist);
+    if (levels > 0) {
+        st_aggregate(&t, W, H, D, sigma_one, costL, dL);
+        levels = ora_st_tree(Rbgr, W, H, tau, t.node, t.parent, t.pdist, t.first, t.nchild, t.cdist);
+    }
+    if (levels > 0) {
+        st_aggregate(&t, W, H, D, sigma_one, costR, dR);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                const int d = dL[y * W + x];
+                int occ = 1;
+                if (x - d >= 0) {
+                    const int dc = dR[y * W + x - d];
+                    occ = (d == 0 || abs(d - dc) > 1);
+                }
+                mask[y * W + x] = (uint8_t)!occ;
+            }
+        levels = ora_st_tree_depth(Lbgr, dL, mask, W, H, D, tau, t.node, t.parent, t.pdist, t.first, t.nchild,
+                                   t.cdist);
+    }
+    if (levels > 0) {
+        st_aggregate(&t, W, H, D, sigma, cost2, out);
+        st_scale(out, P, scale);
+        if (left1) memcpy(left1, dL, (size_t)P);
+        if (right1) memcpy(right1, dR, (size_t)P);
+        if (mask_out) memcpy(mask_out, mask, (size_t)P);
+    }
+    st_tree_free(&t);
+    free(dL);
+    free(dR);
+    free(mask);
+    free(costL);
+    free(costR);
+    free(cost2);
     return levels;
 }

@@ -1,4 +1,4 @@
-"""GPU segment-tree stereo (STMatching ST-1) against the C restatement
+"""GPU segment-tree stereo (STMatching ST-1 and ST-2) against the C restatement
 (oracle/st_oracle.c), bit for bit: the cost, the tree and the filter's float operations are done in
 the reference's order, so the maps are identical, not merely close."""
 import os
@@ -56,3 +56,33 @@ def test_argument_errors(matcher):
         matcher.segment_tree(b, b, 0)
     with pytest.raises(sm.SMError):
         matcher.segment_tree(b, b, 8, 4, 0.0)
+
+
+def test_st2_art_reference_defaults(matcher, oracle):
+    """ST-2 (main.cpp's method 1, stereo_disparity_iteration) on the bundled Art pair at the defaults."""
+    g = np.load(os.path.join(GOLDEN, "middlebury_bgr.npz"))
+    L, R = g["Art/view1"], g["Art/view5"]
+    want, levels, _, _, _ = oracle.st2_disp(L, R, 60, 4, 0.1)
+    got = matcher.segment_tree(L, R, method=1)
+    assert np.array_equal(got, want), int((got != want).sum())
+    tree_ms, total_ms, lv = matcher.segment_tree_stats()
+    assert lv == levels and 0 < tree_ms < total_ms
+    # ST-1 still answers after an ST-2 call on the same handle (shared workspace)
+    want1, _ = oracle.st_disp(L, R, 60, 4, 0.1)
+    assert np.array_equal(matcher.segment_tree(L, R), want1)
+
+
+@pytest.mark.parametrize("W,H,D,scale,sigma,seed", [(97, 61, 16, 1, 0.1, 11), (2, 5, 3, 4, 0.1, 12),
+                                                     (300, 200, 64, 2, 0.08, 13), (123, 1, 9, 3, 0.5, 14),
+                                                     (40, 30, 60, 4, 0.1, 15), (64, 48, 80, 3, 0.005, 16)])
+def test_st2_random_pairs(matcher, oracle, W, H, D, scale, sigma, seed):
+    """ST-2 on textured / flat random pairs: W < D (every right-view pixel takes the repeated-d branch of
+    GetRightMatchingCostFromLeft), a 2-pixel-wide and a 1-row frame, sigma below the 0.01 clamp."""
+    rng = np.random.default_rng(seed)
+    L = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    L[: H // 2, : W // 3] = 77
+    R = np.roll(L, -min(5, W - 1), axis=1)
+    R[:, -3:] = rng.integers(0, 256, (H, min(3, W), 3), dtype=np.uint8)
+    want, _, _, _, _ = oracle.st2_disp(L, R, D, scale, sigma)
+    got = matcher.segment_tree(L, R, D, scale, sigma, method=1)
+    assert np.array_equal(got, want), int((got != want).sum())

@@ -216,3 +216,38 @@ def test_st_recovers_shift(oracle):
     d, levels = oracle.st_disp(L, R, 16, 1, 0.1)
     assert levels > 0
     assert (d[:, 12:] == s).mean() > 0.97
+
+
+def test_st_right_cost_closed_form(oracle):
+    """GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180) as restated equals the closed form the GPU
+    uses: C_R(y, x, d) = C(y, min(x + d, W - 1), min(d, W - 1 - x)), including W < D."""
+    rng = np.random.default_rng(5)
+    for W, H, D in ((50, 12, 16), (9, 4, 20)):
+        L = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        R = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        c = oracle.st_cost(L, R, D)
+        x, d = np.arange(W)[:, None], np.arange(D)[None, :]
+        assert np.array_equal(oracle.st_right_cost(c), c[:, np.minimum(x + d, W - 1), np.minimum(d, W - 1 - x)])
+
+
+def test_st2_pipeline_pieces(oracle):
+    """ST-2's first left map is ST-1 with sigma = SIGMA_ONE (0.08) and scale 1 (StereoDisparity.cpp:115-119),
+    its mask is the left-right check of the two first-pass maps (:129-147), the colour + depth tree spans
+    the image, and the refined map recovers a known shift."""
+    rng = np.random.default_rng(4)
+    H, W, s = 60, 100, 6
+    base = rng.integers(0, 256, (H, W + s, 3), dtype=np.uint8)
+    L, R = base[:, :W].copy(), base[:, s:].copy()
+    out, levels, l1, r1, mk = oracle.st2_disp(L, R, 16, 1, 0.1)
+    assert levels > 0
+    st1, _ = oracle.st_disp(L, R, 16, 1, 0.08)
+    assert np.array_equal(l1, st1)
+    xs = np.arange(W)[None, :].repeat(H, 0)
+    u = xs - l1.astype(int)
+    ok = u >= 0
+    dr = np.where(ok, r1[np.arange(H)[:, None], np.clip(u, 0, W - 1)], 0).astype(int)
+    want = ok & (l1 != 0) & (np.abs(l1.astype(int) - dr) <= 1)
+    assert np.array_equal(mk.astype(bool), want)
+    t = oracle.st_tree_depth(L, l1, mk, 16)
+    assert t["levels"] > 0 and sorted(t["node"].tolist()) == list(range(H * W))
+    assert (out[:, 12:] == s).mean() > 0.97
