@@ -411,10 +411,18 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         chain_step(d);
     };
 
+    // S1V's cs stores and S1H's a/b stores are inline asm, which the compiler's wait-count pass does
+    // not see: where no compiler-visible LDS op is pending (the stats pass, the first d) it issues the
+    // barrier without waiting for them, and another wave can read the rows before they land.  Every
+    // barrier that hands those rows over waits for the LDS queue explicitly.
+    auto lds_barrier = [] {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
     s1v(0, std::true_type{}, std::false_type{});
     const bool s1_nomask = px0 >= D - 1 && px0 >= 0 && px0 + 63 < W;
     const bool s2_lim = valid_mode != 1 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
-    __syncthreads();
+    lds_barrier();
     s1h_stats();
     __syncthreads();
     // buffers: cs (S1V -> S1H), abp (S1H -> S2V), mm (S2V -> S2H); each producer of iteration d+1
@@ -426,14 +434,14 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             else s1v(d, std::false_type{}, std::false_type{});
         }
         if (d > d_lo) s2v();
-        __syncthreads();
+        lds_barrier();
         if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
         if (d < D) s1h();
         if (d > d_lo) {
             if (s2_lim) s2h(d - 1, std::true_type{});
             else s2h(d - 1, std::false_type{});
         }
-        __syncthreads();
+        lds_barrier();
     }
     // drain the right-key chain: 8 SW2 - 1 more steps move every slot out through the last segment
     if constexpr (RIGHT) {

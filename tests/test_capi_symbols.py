@@ -80,3 +80,18 @@ def test_missing_library_fails_loudly(tmp_path):
             _capi.load(str(tmp_path / "nope.so"))
         finally:
             _capi._lib = saved
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc absent")
+def test_asm_lds_stores_are_waited_before_barriers():
+    """The guided kernel writes LDS rows with inline asm (ds_write_addtid_b32, ds_write_b64), which the
+    compiler's wait-count pass does not track.  Every s_barrier after such a store must follow an
+    s_waitcnt lgkmcnt(0), or another wave may read the rows before they land (tools/check_lds_barriers.py
+    on the gfx950 ISA)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("check_lds_barriers",
+                                                  os.path.join(ROOT, "tools", "check_lds_barriers.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    total, bad = mod.check(os.path.join(ROOT, "gpu_stereo_matching_amd", "csrc", "bm_guided.hip"))
+    assert total > 0 and not bad, f"{len(bad)} of {total} barriers follow an unwaited asm LDS store: {sorted(set(bad))[:3]}"

@@ -88,3 +88,10 @@ def test_pair_sequence_order_and_bgr(tmp_path):
         assert np.array_equal(right, frames[n][1][:, :, ::-1])
     small = list(PairSequence(str(tmp_path), size=(3, 2)))
     assert small[0][1].shape == (2, 3, 3)
+
+
+def test_stmatch_usage(capsys):
+    """STMatching's command line prints its usage with fewer than three arguments (main.cpp:41-47)."""
+    from gpu_stereo_matching_amd import stmatch
+    assert stmatch._main([]) == 0
+    assert "leftImgPath rightImgPath dispImgPath" in capsys.readouterr().out
