@@ -22,6 +22,8 @@
 //     (v_sad_u8 / v_sad_hi_u8); CS = T_i - T_{i-2R-1} (column window sums, two d per dword).
 //   Phase H (lane = row x half-row): running window sum along x over the packed pairs, keys
 //     (S << 8 | d) built with v_perm_b32, folded with v_min3_u32.
+#include <cstdlib>
+
 #include "bm_common.h"
 
 namespace sm {
@@ -119,10 +121,12 @@ constexpr uint32_t kSelW = 0x0C0C0504u;
 // for right pixel u = x - d.  Phase H scatter-mins them into a per-tile LDS row (ds_min_u32) that
 // is written to `a.rpart`; right_reduce_lr_kernel folds the ~(TW + D) / TW tiles covering each u.
 // This replaces a second matching pass over the mirrored pair.
-template <int R, int DMAX, bool RIGHT>
-__global__ __launch_bounds__((64 * kWaves<RIGHT, R>), (kMinWavesPerEU<RIGHT, R>))
+// NW = kWideTile (16 waves, one workgroup per CU) for launches of few tiles: the d range of a tile is
+// split over 4x the waves, so a launch of ~1 round of workgroups runs in ~4 short rounds instead.
+constexpr int kWideTile = 16;
+template <int R, int DMAX, bool RIGHT, int NW = kWaves<RIGHT, R>>
+__global__ __launch_bounds__((64 * NW), (NW == kWideTile ? 4 : kMinWavesPerEU<RIGHT, R>))
 void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
-    constexpr int NW = kWaves<RIGHT, R>;
     constexpr int kThreads = 64 * NW;
     using G = Geo<R, DMAX, NW>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -477,6 +481,26 @@ struct RightOut {
     int64_t stride;
 };
 
+int compute_units() {
+    static const int n = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return cus;
+    }();
+    return n;
+}
+
+// SM_WIDE_TILES=0 keeps the 4-wave kernel for every launch (A/B timing)
+bool wide_tiles_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SM_WIDE_TILES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int R, int DMAX, bool RIGHT>
 hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStream_t s) {
     using G = Geo<R, DMAX, kWaves<RIGHT, R>>;
@@ -495,6 +519,19 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
                            tiles_x, tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
                            a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
     } else {
+        // no more tiles than CUs (a small frame, batch 1): 16 waves per tile, >= 2 d-pairs each, so every
+        // CU runs 16 waves instead of <= 4 (R <= 7: the wide-radius kernels need > 128 VGPRs).  Beyond
+        // one tile per CU the 4-wave kernel wins: with one 16-wave workgroup per CU a tile's staging
+        // overlaps no other tile's compute (1080p batch 1: 102.8 vs 87.8 us).
+        const int npairs = ((a.d_hi - a.d_lo + kChunk - 1) & ~(kChunk - 1)) / 2;
+        if constexpr (!kWideR<R>) {
+            if (wide_tiles_enabled() && blocks <= compute_units() && npairs >= 2 * kWideTile) {
+                using GW = Geo<R, DMAX, kWideTile>;
+                hipLaunchKernelGGL((box_match_kernel<R, DMAX, false, kWideTile>), dim3((unsigned)blocks),
+                                   dim3(64 * kWideTile), (size_t)GW::LDS_BYTES, s, a, tiles_x, tiles_y);
+                return hipGetLastError();
+            }
+        }
         hipLaunchKernelGGL((box_match_kernel<R, DMAX, false>), dim3((unsigned)blocks), dim3(64 * kWaves<false, R>),
                            (size_t)G::LDS_BYTES, s, a, tiles_x, tiles_y);
     }
