@@ -599,8 +599,21 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     auto t0 = std::chrono::steady_clock::now();
     HostTree tl, tr;
     bool okR = false;
-    std::thread th([&] { okR = build_tree(hw.data() + 2 * P, hw.data() + 3 * P, W, H, tau, tr); });
-    const bool okL = build_tree(hw.data(), hw.data() + P, W, H, tau, tl);
+    // neither build may leave its exception behind the other's thread (a joinable std::thread must not
+    // be destroyed): a failed build reports false
+    std::thread th([&] {
+        try {
+            okR = build_tree(hw.data() + 2 * P, hw.data() + 3 * P, W, H, tau, tr);
+        } catch (...) {
+            okR = false;
+        }
+    });
+    bool okL = false;
+    try {
+        okL = build_tree(hw.data(), hw.data() + P, W, H, tau, tl);
+    } catch (...) {
+        okL = false;
+    }
     th.join();
     if (!okL || !okR) return hipErrorInvalidValue;
     float tab1[256];

@@ -1104,15 +1104,23 @@ int segment_tree_call(sm_handle* h, const uint8_t* left_bgr, const uint8_t* righ
 SM_API int sm_segment_tree_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
                                         int height, int pitch, int max_level, int scale, float sigma,
                                         uint8_t* disp_out, int out_pitch) {
-    return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
-                             out_pitch, false);
+    try {
+        return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
+                                 out_pitch, false);
+    } catch (const std::bad_alloc&) {   // the host tree's buffers: no C++ exception crosses the C ABI
+        return fail(SM_ERR_OUT_OF_MEMORY, "segment tree: host allocation failed");
+    }
 }
 
 SM_API int sm_segment_tree_refined_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
                                           int height, int pitch, int max_level, int scale, float sigma,
                                           uint8_t* disp_out, int out_pitch) {
-    return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
-                             out_pitch, true);
+    try {
+        return segment_tree_call(h, left_bgr, right_bgr, width, height, pitch, max_level, scale, sigma, disp_out,
+                                 out_pitch, true);
+    } catch (const std::bad_alloc&) {
+        return fail(SM_ERR_OUT_OF_MEMORY, "segment tree: host allocation failed");
+    }
 }
 
 SM_API int sm_last_segment_tree_stats(sm_handle* h, float* tree_ms, float* total_ms, int* levels) {
