@@ -6,7 +6,7 @@ import csv, glob, json, os, subprocess, sys, statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "box_r5_1080p"
 W, H, D, r = 1920, 1080, 128, 5
-B = int(os.environ.get("SM_PMC_BATCH", "32"))   # bench.py's default frames per step
+B = int(os.environ.get("SM_PMC_BATCH", "128"))   # bench.py's default frames per step
 out = os.path.join(ROOT, "gpurun_out", "pmc_" + tag)
 env = dict(os.environ, TMPDIR="/tmp")
 vals = {}

@@ -1,7 +1,7 @@
 """VALU / LDS instruction counts per launch of the bench's compute-bound kernels, for bench.py's
 `roofline` (bound "valu").  One rocprofv3 --pmc pass per workload (SQ counters only, no tracing
 domains: MI355X_MICROARCH.md §PMC), on tools/kernel_driver.py with the bench's exact configuration
-(1080p D=128 r=5, 32 frames per launch).  SQ_INSTS_VALU is a chip total of wave64 instructions and
+(1080p D=128 r=5; the box kernel at the headline's 128 frames per launch, guided at 32).  SQ_INSTS_VALU is a chip total of wave64 instructions and
 does not depend on timing, so bench.py divides it by the live HIP-event kernel time.
 
     python tools/valu_counts.py            # writes profiles/valu_counts.json
@@ -12,7 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CTRS = "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
 # name, kernel-name substring, driver args; workload = [W, H, D, r, frames per launch]
 JOBS = (
-    ("box_r5_1080p_d128_b32", "box_match_kernel<5, 128, false>", ["--agg", "box", "--batch", "32"], [1920, 1080, 128, 5, 32]),
+    ("box_r5_1080p_d128_b128", "box_match_kernel<5, 128, false, 4>", ["--agg", "box", "--batch", "128"],
+     [1920, 1080, 128, 5, 128]),
     ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false>", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
     ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true>", ["--agg", "guided", "--lr", "--batch", "32"],
      [1920, 1080, 128, 5, 32]),
