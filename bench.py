@@ -124,10 +124,10 @@ def cpu_baseline(W, H, D, r, seed):
 VARIANTS = (
     # name, W, H, D, r, agg, lr, median, batch
     # cfg1 / cfg2 on the reference's own bundled Middlebury pairs (Art, Books, Dolls; gray fixtures
-    # in tests/golden, 463x370 — BASELINE's "450x375"), cycled to 16 frames per launch
-    ("cfg1 Middlebury Art/Books/Dolls 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, False, 16),
-    ("cfg2 Middlebury Art/Books/Dolls 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, False, 16),
-    # 1080p variants run 32 frames per launch like the headline, 4K 8 (the same ~8 rounds of
+    # in tests/golden, 463x370 — BASELINE's "450x375"), cycled to 96 frames per launch (9216 tiles, 9 rounds)
+    ("cfg1 Middlebury Art/Books/Dolls 463x370 7x7 box d64", 463, 370, 64, 3, "box", False, False, 96),
+    ("cfg2 Middlebury Art/Books/Dolls 463x370 9x9 box d64", 463, 370, 64, 4, "box", False, False, 96),
+    # 1080p variants run 32 frames per launch, 4K 8 (the same ~38 rounds of
     # workgroups per launch): 4-frame launches lose 12-14 % to each launch's ramp-down
     ("cfg3 1080p 11x11 box+lr d128", 1920, 1080, 128, 5, "box", True, False, 32),
     ("cfg3 1080p 11x11 box+median7+lr d128", 1920, 1080, 128, 5, "box", True, True, 32),
