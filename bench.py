@@ -273,6 +273,21 @@ def run_variants(sm, torch, dev, stream, seed):
             up, mt, dn = m.stage_ms()
             out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
                          "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+            # the same call on caller frames / map in sm_host_alloc (page-locked) memory
+            Lp, Rp, Op = sm.host_empty((H, W)), sm.host_empty((H, W)), sm.host_empty((H, W))
+            Lp[...] = L
+            Rp[...] = R
+            for _ in range(3):
+                m.match(Lp, Rp, r, D, out=Op)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                m.match(Lp, Rp, r, D, out=Op)
+            ms = (time.perf_counter() - t0) * 1000 / n
+            up, mt, dn = m.stage_ms()
+            out[name + " (sm_host_alloc buffers)"] = {
+                "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
+                "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+            del Lp, Rp, Op
         # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's
         # defaults: a synchronous host call (host tree builds + GPU cost / filter / WTA / median / LR check), wall
         g = np.load(os.path.join(ROOT, "tests", "golden", "middlebury_bgr.npz"))

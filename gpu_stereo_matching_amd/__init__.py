@@ -28,7 +28,7 @@ from .gray import bgr_to_gray  # noqa: F401
 
 __all__ = [
     "BlockMatcher", "BlockMatcherGroup", "blockMatching_gpu", "block_matching_gpu", "SMError", "synth_pair", "bgr_to_gray",
-    "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "SM_MEDIAN", "version",
+    "SM_AGG_BOX", "SM_AGG_GUIDED", "SM_LR_CHECK", "SM_MEDIAN", "version", "host_empty",
 ]
 
 DEFAULT_GUIDED_EPS = 1e-4 * 255.0 * 255.0
@@ -73,6 +73,33 @@ def _check_device_pair(left_t, right_t, keys_t=None):
     if keys_t is not None and (keys_t.dtype != torch.int32 or tuple(keys_t.shape) != tuple(left_t.shape)
                                or not keys_t.is_contiguous() or keys_t.device != left_t.device):
         raise ValueError("keys_t must be a contiguous int32 [H, W] tensor on the frames' device")
+
+
+class _PinnedBlock:
+    """Owner of one sm_host_alloc block; freed when the last array viewing it goes away."""
+
+    def __init__(self, nbytes: int):
+        self._lib = _capi.load()
+        p = ctypes.c_void_p()
+        _capi.check(self._lib.sm_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.sm_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def host_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """An uninitialised numpy array in page-locked host memory (``sm_host_alloc``): frames and maps
+    kept here go to / from HBM as direct DMA in ``BlockMatcher.match`` and friends."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    blk = _PinnedBlock(max(n, 1))
+    buf = (ctypes.c_uint8 * max(n, 1)).from_address(blk.ptr)
+    buf._sm_owner = blk  # the ctypes buffer keeps the block alive, and the array keeps the buffer
+    return np.frombuffer(buf, dtype=dt, count=n // dt.itemsize).reshape(shape)
 
 
 class BlockMatcher:

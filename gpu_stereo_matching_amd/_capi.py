@@ -38,7 +38,7 @@ EXPORTED = (
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
     "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_segment_tree_refined_bgr_u8",
-    "sm_last_segment_tree_stats",
+    "sm_last_segment_tree_stats", "sm_host_alloc", "sm_host_free",
 )
 
 
@@ -87,6 +87,8 @@ def load(path: str = LIB_PATH):
     L.sm_guided_slice_keys_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, vp, vp]
     L.sm_guided_keys_to_disp_device.argtypes = [vp, vp, i, i, vp, i, vp]
     L.sm_stream_sync.argtypes = [vp, vp]
+    L.sm_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.sm_host_free.argtypes = [vp]
     L.sm_median_u8_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
     L.sm_bgr_to_gray_u8.argtypes = [vp, vp, i, i, i, i, vp, i]
     L.sm_remap_u8.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i]

@@ -726,6 +726,21 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
     return fail(SM_ERR_INVALID_ARG, "unknown param %d", param);
 }
 
+SM_API int sm_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "null out pointer");
+    *out = nullptr;
+    if (bytes == 0) return fail(SM_ERR_INVALID_ARG, "zero-byte host allocation");
+    // portable: usable by every device's handle (a group's members copy from one frame)
+    SM_HIP(hipHostMalloc(out, bytes, hipHostMallocPortable));
+    return SM_OK;
+}
+
+SM_API int sm_host_free(void* p) {
+    if (!p) return SM_OK;
+    SM_HIP(hipHostFree(p));
+    return SM_OK;
+}
+
 SM_API int sm_block_match_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
                              int pitch, int radius, int num_disp, unsigned flags, uint8_t* disp_out, int out_pitch) {
     return host_match(h, left, right, width, height, pitch, radius, num_disp, flags, disp_out, nullptr, nullptr,

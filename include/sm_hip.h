@@ -69,11 +69,18 @@ SM_API const char *sm_last_error_string(void);      /* thread-local message of t
 SM_API int sm_device_count(int *count);
 
 /* Create a handle on HIP device `device`, sized for frames up to max_width x max_height and
- * up to max_disp disparities (1..256).  Device buffers and pinned staging are allocated once
- * here (the reference re-allocates and leaks ~2*P*D bytes per call: Device.cu:185-194). */
+ * up to max_disp disparities (1..256).  Device frame buffers are allocated once here (the
+ * reference re-allocates and leaks ~2*P*D bytes per call: Device.cu:185-194). */
 SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm_handle **out);
 SM_API int sm_destroy(sm_handle *h);
 SM_API int sm_set_param_f(sm_handle *h, int param, float value);
+
+/* Page-locked host memory for frames and maps (hipHostMalloc, portable).  The host entry points
+ * take any host pointer; with buffers from here their copies run as DMA straight from / into the
+ * caller's memory instead of through the runtime's pageable bounce buffers (the reference's
+ * Mat data is pageable: Device.cu:212-216, 287-291).  sm_host_free(NULL) is a no-op. */
+SM_API int sm_host_alloc(size_t bytes, void **out);
+SM_API int sm_host_free(void *p);
 
 /* Host-pointer entry point — the blockMatching_gpu replacement.
  * left/right: uint8 gray, `height` rows of `width` bytes at row stride `pitch` (>= width).

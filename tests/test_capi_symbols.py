@@ -95,3 +95,14 @@ def test_asm_lds_stores_are_waited_before_barriers():
     spec.loader.exec_module(mod)
     total, bad = mod.check(os.path.join(ROOT, "gpu_stereo_matching_amd", "csrc", "bm_guided.hip"))
     assert total > 0 and not bad, f"{len(bad)} of {total} barriers follow an unwaited asm LDS store: {sorted(set(bad))[:3]}"
+
+
+def test_host_alloc_rejects_bad_args():
+    """sm_host_alloc validates its arguments before touching the HIP runtime."""
+    import ctypes
+    from gpu_stereo_matching_amd import _capi
+    L = _capi.load()
+    assert L.sm_host_alloc(16, None) != 0
+    p = ctypes.c_void_p()
+    assert L.sm_host_alloc(0, ctypes.byref(p)) != 0 and not p.value
+    assert L.sm_host_free(None) == 0

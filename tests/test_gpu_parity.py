@@ -595,3 +595,20 @@ def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
             k = p if k is None else torch.minimum(k, p)
         torch.cuda.synchronize()
         assert np.array_equal(k.cpu().numpy().view(np.uint32), keys), (W, H, r, D, cuts)
+
+
+def test_pinned_host_buffers(sm, matcher, oracle):
+    """sm_host_alloc frames and maps through the drop-in host path (DMA straight from / into the
+    caller's page-locked memory) give the same maps as pageable numpy buffers."""
+    W, H, D, r = 1920, 1080, 128, 5
+    L, R = oracle.synth_pair(41, W, H, D)
+    want = oracle.box_disp(L, R, r, D)
+    Lp, Rp, Op = sm.host_empty((H, W)), sm.host_empty((H, W)), sm.host_empty((H, W))
+    Lp[...] = L
+    Rp[...] = R
+    Op[...] = 7
+    got = matcher.match(Lp, Rp, r, D, out=Op)
+    assert got is Op and np.array_equal(Op, want)
+    chk, rd, mask = matcher.match_lr(Lp, Rp, r, D)
+    _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, r, D)
+    assert np.array_equal(chk, chk_o) and np.array_equal(rd, rd_o) and np.array_equal(mask, mask_o)
