@@ -612,3 +612,19 @@ def test_pinned_host_buffers(sm, matcher, oracle):
     chk, rd, mask = matcher.match_lr(Lp, Rp, r, D)
     _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, r, D)
     assert np.array_equal(chk, chk_o) and np.array_equal(rd, rd_o) and np.array_equal(mask, mask_o)
+
+
+@pytest.mark.parametrize("W,H,D,r", [(333, 257, 64, 7), (640, 256, 96, 0), (500, 300, 128, 11),
+                                     (1001, 400, 256, 15), (320, 260, 32, 3)])
+def test_pinned_odd_shapes(sm, matcher, oracle, W, H, D, r):
+    """Page-locked frames through the host path at odd heights, r = 0, the r > 7 kernel, with
+    pageable and page-locked outputs: bit-exact with the oracle and with pageable frames."""
+    L, R = oracle.synth_pair(50 + r, W, H, D)
+    want = oracle.box_disp(L, R, r, D)
+    Lp, Rp = sm.host_empty((H, W)), sm.host_empty((H, W))
+    Lp[...] = L
+    Rp[...] = R
+    assert np.array_equal(matcher.match(Lp, Rp, r, D), want)           # pageable output
+    Op = sm.host_empty((H, W))
+    assert np.array_equal(matcher.match(Lp, Rp, r, D, out=Op), want)   # pinned output
+    assert np.array_equal(matcher.match(L, R, r, D), want)             # pageable frames: one-piece path
