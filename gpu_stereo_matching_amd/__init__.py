@@ -134,6 +134,22 @@ class BlockMatcher:
     def set_guided_eps(self, eps: float):
         _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_GUIDED_EPS, float(eps)))
 
+    def dslice_rehearse(self, left, right, radius: int, num_disp: int, members: int, agg: str = "box") -> np.ndarray:
+        """The d-slice split of BlockMatcherGroup.match_dslice with `members` members, run one after
+        another on this device (sm_dslice_rehearse_u8): same slice plan, padding and finalisation, with
+        the RCCL MIN reduce-scatter replaced by an elementwise MIN of the members' key maps."""
+        if agg not in ("box", "guided"):
+            raise ValueError("agg must be 'box' or 'guided'")
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        if L.shape != R.shape:
+            raise ValueError("left/right sizes differ")
+        H, W = L.shape
+        out = np.empty((H, W), np.uint8)
+        _capi.check(self._lib.sm_dslice_rehearse_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
+                                                    _flags(agg, False, False), members, out.ctypes.data, W))
+        return out
+
     # -- host-pointer path (blockMatching_gpu replacement) -------------------------------
     def match(self, left, right, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,
               median: bool = False, out: Optional[np.ndarray] = None) -> np.ndarray:

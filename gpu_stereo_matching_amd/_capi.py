@@ -25,6 +25,7 @@ SM_MEDIAN = 4
 SM_STAGED = 8
 
 SM_PARAM_GUIDED_EPS = 1
+SM_PARAM_STAGED_GROUP = 2
 
 # every symbol include/sm_hip.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = (
@@ -38,7 +39,7 @@ EXPORTED = (
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
     "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_segment_tree_refined_bgr_u8",
-    "sm_last_segment_tree_stats", "sm_host_alloc", "sm_host_free",
+    "sm_last_segment_tree_stats", "sm_host_alloc", "sm_host_free", "sm_dslice_plan", "sm_dslice_rehearse_u8",
 )
 
 
@@ -113,6 +114,9 @@ def load(path: str = LIB_PATH):
     L.sm_group_block_match_lr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, vp, vp, i]
     L.sm_group_block_match_batch_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]
     L.sm_group_dslice_block_match_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, vp, i]
+    L.sm_dslice_plan.argtypes = [i64, i, i, i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i64),
+                                 ctypes.POINTER(i64)]
+    L.sm_dslice_rehearse_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, i, vp, i]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

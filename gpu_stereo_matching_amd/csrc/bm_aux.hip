@@ -55,7 +55,20 @@ __global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* ld, int lp
     if (right_out) right_out[(int64_t)f * astride + (int64_t)y * apitch + x] = rrow[mirrored ? W - 1 - x : x];
 }
 
+// acc[i] = min(acc[i], src[i]), signed (box keys are < 2^31, guided keys carry a signed cost): the
+// MIN of an RCCL reduce-scatter, for the d-slice split rehearsed on one device (sm_dslice_rehearse_u8)
+__global__ __launch_bounds__(256) void min_keys_kernel(int* __restrict__ acc, const int* __restrict__ src, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) acc[i] = min(acc[i], src[i]);
+}
+
 }  // namespace
+
+hipError_t launch_min_keys(int* acc, const int* src, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(min_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, src, n);
+    return hipGetLastError();
+}
 
 hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key, uint8_t* disp,
                                int out_pitch, hipStream_t s) {

@@ -50,6 +50,8 @@ hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t
 size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch);
 hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key,
                                uint8_t* disp, int out_pitch, hipStream_t s);
+// acc = min(acc, src) elementwise over n signed keys (the d-slice MIN, rehearsed on one device)
+hipError_t launch_min_keys(int* acc, const int* src, int64_t n, hipStream_t s);
 hipError_t launch_mirror(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch,
                          uint8_t* dst, int dst_pitch, int64_t dst_stride, hipStream_t s);
 // right_mirrored: 1 if the right map is stored mirrored (index W-1-u holds dR(u)), 0 if plain

@@ -9,6 +9,8 @@
 //   * any frame size works (the reference's fixed (8,10,D)x(32,32) grid covers 320x256 only, :231-233).
 #include <dlfcn.h>
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <cstdio>
@@ -55,6 +57,7 @@ struct sm_handle {
     uint8_t* d_bgr = nullptr;
     size_t bgr_bytes = 0;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
+    int staged_group = 8;        // SM_STAGED frames per launch group (SM_PARAM_STAGED_GROUP)
     // The workspaces above are shared by every call on the handle while calls run on the stream
     // they are given: the end of each pass is recorded here, and a pass on another stream waits
     // for it first, so two streams never write the same workspace at once.
@@ -187,7 +190,7 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     const int64_t P = (int64_t)W * H;
     if (W > 4096) return fail(SM_ERR_INVALID_ARG, "SM_STAGED: width %d exceeds 4096", W);
     const int64_t per_frame = 3 * P * D + (med ? P : 0);
-    int group = (int)std::min<int64_t>(kStagedGroup, std::max<int64_t>(1, kStagedBytes / per_frame));
+    int group = (int)std::min<int64_t>(h->staged_group, std::max<int64_t>(1, kStagedBytes / per_frame));
     group = std::min(group, std::max(batch, 1));
     int rc = ensure_vol(h, (size_t)(per_frame * group));
     if (rc) return rc;
@@ -485,6 +488,8 @@ struct RcclApi {
     decltype(&ncclReduceScatter) reduce_scatter;
     decltype(&ncclAllGather) all_gather;
     decltype(&ncclGetErrorString) error_string;
+    decltype(&ncclCommAbort) abort;
+    decltype(&ncclCommGetAsyncError) async_error;
 };
 
 const RcclApi* rccl_api() {
@@ -502,7 +507,11 @@ const RcclApi* rccl_api() {
             api.reduce_scatter = reinterpret_cast<decltype(api.reduce_scatter)>(dlsym(lib, "ncclReduceScatter"));
             api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(lib, "ncclAllGather"));
             api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(lib, "ncclGetErrorString"));
-            if (api.init_all && api.destroy && api.reduce_scatter && api.all_gather && api.error_string) state = 1;
+            api.abort = reinterpret_cast<decltype(api.abort)>(dlsym(lib, "ncclCommAbort"));
+            api.async_error = reinterpret_cast<decltype(api.async_error)>(dlsym(lib, "ncclCommGetAsyncError"));
+            if (api.init_all && api.destroy && api.reduce_scatter && api.all_gather && api.error_string && api.abort &&
+                api.async_error)
+                state = 1;
         }
     }
     return state == 1 ? &api : nullptr;
@@ -534,67 +543,173 @@ int group_comms(sm_group* g) {
     return SM_OK;
 }
 
-// One member's share of a d-sliced frame (runs on that member's worker thread): upload the pair,
-// slice keys over [lo, hi), MIN reduce-scatter of the int32 keys, finalise this member's pixel
-// chunk to uint8, all-gather the chunks; member 0 downloads the map.
-int dslice_member(sm_handle* h, ncclComm_t comm, int k, int n, const uint8_t* left, const uint8_t* right, int W,
-                  int H, int pitch, int radius, int D, bool guided, uint8_t* disp_out, int out_pitch) {
-    const RcclApi* api = rccl_api();
+// ---- the d-slice split (sm_group_dslice_block_match_u8, sm_dslice_rehearse_u8) ----
+// One plan for every path that shards a frame over d: the C group call, its one-device rehearsal and
+// the torch path (sharding.py calls sm_dslice_plan).  Member k of n scans d in [kD/n, (k+1)D/n)
+// (Device.cu:43-61: the d planes are independent); the P keys are padded with the "no match" key to
+// Ppad = n * chunk so that the MIN reduce-scatter hands member k the pixels [k*chunk, (k+1)*chunk),
+// and the all-gather puts chunk k back at offset k*chunk.
+struct DslicePlan {
+    int lo, hi;
+    int64_t chunk, padded;
+};
+
+DslicePlan dslice_plan(int64_t P, int D, int n, int k) {
+    DslicePlan p;
+    p.lo = (int)((int64_t)k * D / n);
+    p.hi = (int)((int64_t)(k + 1) * D / n);
+    p.chunk = (P + n - 1) / n;
+    p.padded = p.chunk * n;
+    return p;
+}
+
+// keys no d of the slice improves: the Device.cu:37 seed (box) / INT32_MAX (guided, signed keys)
+uint32_t dslice_none_key(int radius, bool guided) { return guided ? 0x7FFFFFFFu : seed_key(radius); }
+
+int ensure_dsl(sm_handle* h, size_t need) {
+    if (h->dsl_bytes >= need) return SM_OK;
+    if (h->d_dsl) (void)hipFree(h->d_dsl);
+    h->d_dsl = nullptr;
+    h->dsl_bytes = 0;
+    SM_HIP(hipMalloc(&h->d_dsl, need));
+    h->dsl_bytes = need;
+    return SM_OK;
+}
+
+// Test hook (include/sm_hip.h): SM_DSLICE_FAULT="<member>:<phase>" makes that member fail in phase
+// "keys" (before any collective) or "collective" (instead of enqueuing its reduce-scatter).
+bool dslice_fault(int k, const char* phase) {
+    const char* e = getenv("SM_DSLICE_FAULT");
+    if (!e) return false;
+    const char* colon = strchr(e, ':');
+    return colon && atoi(e) == k && strcmp(colon + 1, phase) == 0;
+}
+
+// Member-side key pass over its slice: keys[0, padded) on stream s from the frames already on the
+// device (d_left / d_right, pitch W).
+int dslice_keys(sm_handle* h, const DslicePlan& p, int W, int H, int radius, bool guided, uint32_t* keys,
+                hipStream_t s) {
     const int64_t P = (int64_t)W * H;
-    const int64_t chunk = (P + n - 1) / n, Ppad = chunk * n;
-    const size_t need = (size_t)(Ppad * 4 + chunk * 4 + chunk + Ppad);
-    SM_HIP(hipSetDevice(h->device));
-    hipStream_t s = h->stream;
-    if (h->dsl_bytes < need) {
-        if (h->d_dsl) (void)hipFree(h->d_dsl);
-        h->d_dsl = nullptr;
-        h->dsl_bytes = 0;
-        SM_HIP(hipMalloc(&h->d_dsl, need));
-        h->dsl_bytes = need;
-    }
-    uint32_t* keys = reinterpret_cast<uint32_t*>(h->d_dsl);
-    uint32_t* mine = keys + Ppad;
-    uint8_t* mine8 = reinterpret_cast<uint8_t*>(mine + chunk);
-    uint8_t* map = mine8 + chunk;
-    SM_HIP(copy2d(h->d_left, W, left, pitch, W, H, hipMemcpyHostToDevice, s));
-    SM_HIP(copy2d(h->d_right, W, right, pitch, W, H, hipMemcpyHostToDevice, s));
-    // keys no d of the slice improves: the Device.cu:37 seed (box) / INT32_MAX (guided, signed keys)
-    const uint32_t none = guided ? 0x7FFFFFFFu : seed_key(radius);
-    const int lo = (int)((int64_t)k * D / n), hi = (int)((int64_t)(k + 1) * D / n);
-    if (Ppad > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(Ppad - P), s));
-    if (hi > lo) {
-        if (guided) {
-            SM_HIP(sm::launch_guided_slice_keys(h->d_left, h->d_right, W, H, W, 1, P, radius, lo, hi, h->guided_eps,
-                                                reinterpret_cast<int*>(keys), s));
-        } else {
-            sm::MatchArgs a{};
-            a.left = h->d_left;
-            a.right = h->d_right;
-            a.W = W;
-            a.H = H;
-            a.pitch = W;
-            a.frame_stride = P;
-            a.radius = radius;
-            a.d_lo = lo;
-            a.d_hi = hi;
-            a.valid_mode = 0;
-            a.seed_key = seed_key(radius);
-            a.thresh_key = seed_key(radius);
-            a.keys = keys;
-            SM_HIP(sm::launch_box_match(a, 1, s));
-        }
-    } else {
+    const uint32_t none = dslice_none_key(radius, guided);
+    if (p.padded > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(p.padded - P), s));
+    if (p.hi <= p.lo) {   // more members than disparities: an empty slice contributes "no match"
         SM_HIP(hipMemsetD32Async(keys, (int)none, (size_t)P, s));
+        return SM_OK;
     }
-    // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
-    SM_RCCL(api, api->reduce_scatter(keys, mine, (size_t)chunk, guided ? ncclInt32 : ncclUint32, ncclMin, comm, s));
+    if (guided) {
+        SM_HIP(sm::launch_guided_slice_keys(h->d_left, h->d_right, W, H, W, 1, P, radius, p.lo, p.hi, h->guided_eps,
+                                            reinterpret_cast<int*>(keys), s));
+        return SM_OK;
+    }
+    sm::MatchArgs a{};
+    a.left = h->d_left;
+    a.right = h->d_right;
+    a.W = W;
+    a.H = H;
+    a.pitch = W;
+    a.frame_stride = P;
+    a.radius = radius;
+    a.d_lo = p.lo;
+    a.d_hi = p.hi;
+    a.valid_mode = 0;
+    a.seed_key = seed_key(radius);
+    a.thresh_key = seed_key(radius);
+    a.keys = keys;
+    SM_HIP(sm::launch_box_match(a, 1, s));
+    return SM_OK;
+}
+
+// A reduced key chunk -> uint8 (the Device.cu:37 threshold, after the MIN)
+int dslice_finalise(const uint32_t* mine, int64_t chunk, int radius, bool guided, uint8_t* mine8, hipStream_t s) {
     if (guided)
         SM_HIP(sm::launch_guided_keys_to_disp(reinterpret_cast<const int*>(mine), (int)chunk, 1, mine8, (int)chunk, s));
     else
         SM_HIP(sm::launch_keys_to_disp(mine, (int)chunk, 1, seed_key(radius), mine8, (int)chunk, s));
-    SM_RCCL(api, api->all_gather(mine8, map, (size_t)chunk, ncclUint8, comm, s));
-    if (k == 0) SM_HIP(copy2d(disp_out, out_pitch, map, W, W, H, hipMemcpyDeviceToHost, s));
+    return SM_OK;
+}
+
+// Member workspace: keys [padded] | reduced chunk [chunk] | uint8 chunk [chunk] | gathered map [padded]
+struct DsliceWs {
+    uint32_t* keys;
+    uint32_t* mine;
+    uint8_t* mine8;
+    uint8_t* map;
+};
+DsliceWs dslice_ws(sm_handle* h, const DslicePlan& p) {
+    DsliceWs w;
+    w.keys = reinterpret_cast<uint32_t*>(h->d_dsl);
+    w.mine = w.keys + p.padded;
+    w.mine8 = reinterpret_cast<uint8_t*>(w.mine + p.chunk);
+    w.map = w.mine8 + p.chunk;
+    return w;
+}
+
+// Phase 1 of member k (its worker thread): workspace, upload, slice keys, and a stream sync so that
+// every local failure (allocation, copy, launch, kernel fault) is known before any member enqueues a
+// collective.  A member that fails here returns before phase 2 starts, so nobody waits on it.
+int dslice_member_keys(sm_handle* h, int k, int n, const uint8_t* left, const uint8_t* right, int W, int H, int pitch,
+                       int radius, int D, bool guided) {
+    const int64_t P = (int64_t)W * H;
+    const DslicePlan p = dslice_plan(P, D, n, k);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    if (dslice_fault(k, "keys")) return fail(SM_ERR_LAUNCH, "d-slice member %d: injected fault (keys)", k);
+    int rc = ensure_dsl(h, (size_t)(p.padded * 4 + p.chunk * 4 + p.chunk + p.padded));
+    if (rc) return rc;
+    const DsliceWs w = dslice_ws(h, p);
+    SM_HIP(copy2d(h->d_left, W, left, pitch, W, H, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, W, right, pitch, W, H, hipMemcpyHostToDevice, s));
+    rc = dslice_keys(h, p, W, H, radius, guided, w.keys, s);
+    if (rc) return rc;
     SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
+}
+
+// Shared by the members of one phase-2 call: a member that cannot take part raises `abort`, and
+// every member then aborts its communicator instead of waiting for the missing peer.
+struct DsliceSync {
+    std::atomic<bool> abort{false};
+};
+
+// Phase 2 of member k: MIN reduce-scatter, finalise, all-gather, member 0 downloads.  Waits by
+// polling its stream and the shared abort flag (and RCCL's async error), so that no member blocks
+// forever on a collective a failed peer never joined (the ncclCommAbort pattern).  On any failure
+// the member's communicator is aborted and its slot set to null (the group re-creates them).
+int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, DsliceSync* sync, int k, int n, int W,
+                          int H, int radius, int D, bool guided, uint8_t* disp_out, int out_pitch) {
+    const int64_t P = (int64_t)W * H;
+    const DslicePlan p = dslice_plan(P, D, n, k);
+    const DsliceWs w = dslice_ws(h, p);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    auto bail = [&](int code, const char* what) {
+        sync->abort.store(true);
+        (void)api->abort(*comm);
+        *comm = nullptr;
+        return fail(code, "d-slice member %d: %s", k, what);
+    };
+    if (dslice_fault(k, "collective")) return bail(SM_ERR_LAUNCH, "injected fault (collective)");
+    // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
+    if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, guided ? ncclInt32 : ncclUint32, ncclMin, *comm, s) !=
+        ncclSuccess)
+        return bail(SM_ERR_LAUNCH, "ncclReduceScatter failed");
+    if (dslice_finalise(w.mine, p.chunk, radius, guided, w.mine8, s)) return bail(SM_ERR_LAUNCH, "finalise launch failed");
+    if (api->all_gather(w.mine8, w.map, (size_t)p.chunk, ncclUint8, *comm, s) != ncclSuccess)
+        return bail(SM_ERR_LAUNCH, "ncclAllGather failed");
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return bail(SM_ERR_LAUNCH, hipGetErrorString(q));
+        ncclResult_t async = ncclSuccess;
+        if (api->async_error(*comm, &async) != ncclSuccess || async != ncclSuccess)
+            return bail(SM_ERR_LAUNCH, "RCCL asynchronous error");
+        if (sync->abort.load()) return bail(SM_ERR_LAUNCH, "aborted: another member failed");
+        std::this_thread::yield();
+    }
+    if (k == 0) {
+        SM_HIP(copy2d(disp_out, out_pitch, w.map, W, W, H, hipMemcpyDeviceToHost, s));
+        SM_HIP(hipStreamSynchronize(s));
+    }
     return SM_OK;
 }
 
@@ -720,6 +835,13 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
     if (param == SM_PARAM_GUIDED_EPS) {
         if (!(value > 0.f)) return fail(SM_ERR_INVALID_ARG, "guided eps must be > 0");
         h->guided_eps = value;
+        return SM_OK;
+    }
+    if (param == SM_PARAM_STAGED_GROUP) {
+        const int g = (int)value;
+        if ((float)g != value || g < 1 || g > kStagedGroup)
+            return fail(SM_ERR_INVALID_ARG, "staged launch group must be an integer in [1, %d]", kStagedGroup);
+        h->staged_group = g;
         return SM_OK;
     }
 
@@ -1306,16 +1428,95 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
     int rc = group_comms(g);
     if (rc) return rc;
     const int n = (int)g->w.size();
+    // phase 1 on every member: upload + slice keys, stream synchronised (no collective yet)
     std::vector<std::function<int()>> jobs;
     for (int k = 0; k < n; ++k) {
         sm_handle* h = g->w[k]->h;
-        ncclComm_t c = g->comms[k];
         jobs.push_back([=]() -> int {
-            return dslice_member(h, c, k, n, left, right, width, height, pitch, radius, num_disp, guided, disp_out,
-                                 out_pitch);
+            return dslice_member_keys(h, k, n, left, right, width, height, pitch, radius, num_disp, guided);
         });
     }
-    return group_run(g, jobs);
+    rc = group_run(g, jobs);
+    if (rc) return rc;
+    // phase 2: the collectives, entered by every member or aborted by all
+    const RcclApi* api = rccl_api();
+    DsliceSync sync;
+    jobs.clear();
+    for (int k = 0; k < n; ++k) {
+        sm_handle* h = g->w[k]->h;
+        ncclComm_t* c = &g->comms[k];
+        DsliceSync* sy = &sync;
+        jobs.push_back([=]() -> int {
+            return dslice_member_collect(h, api, c, sy, k, n, width, height, radius, num_disp, guided, disp_out,
+                                         out_pitch);
+        });
+    }
+    rc = group_run(g, jobs);
+    if (sync.abort.load()) {   // some communicators were aborted: drop the rest, re-create on next use
+        for (ncclComm_t& c : g->comms)
+            if (c) (void)api->destroy(c);
+        g->comms.clear();
+    }
+    return rc;
+}
+
+SM_API int sm_dslice_plan(int64_t pixels, int num_disp, int members, int member, int* d_lo, int* d_hi,
+                          int64_t* chunk, int64_t* padded_pixels) {
+    if (pixels <= 0 || num_disp < 1 || members < 1 || member < 0 || member >= members)
+        return fail(SM_ERR_INVALID_ARG, "d-slice plan: pixels %lld, num_disp %d, member %d of %d", (long long)pixels,
+                    num_disp, member, members);
+    const DslicePlan p = dslice_plan(pixels, num_disp, members, member);
+    if (d_lo) *d_lo = p.lo;
+    if (d_hi) *d_hi = p.hi;
+    if (chunk) *chunk = p.chunk;
+    if (padded_pixels) *padded_pixels = p.padded;
+    return SM_OK;
+}
+
+SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                                 int pitch, int radius, int num_disp, unsigned flags, int members, uint8_t* disp_out,
+                                 int out_pitch) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (out_pitch < width) return fail(SM_ERR_INVALID_ARG, "out_pitch %d < width %d", out_pitch, width);
+    if (members < 1 || members > 64) return fail(SM_ERR_INVALID_ARG, "members %d out of [1, 64]", members);
+    if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
+        return fail(SM_ERR_INVALID_ARG, "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED only)", flags);
+    const bool guided = (flags & SM_AGG_GUIDED) != 0;
+    if (guided && radius > sm::kMaxFastRadius)
+        return fail(SM_ERR_INVALID_ARG, "guided aggregation: radius %d > %d", radius, sm::kMaxFastRadius);
+    if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
+    const int64_t P = (int64_t)width * height;
+    const int n = members;
+    const DslicePlan p0 = dslice_plan(P, num_disp, n, 0);
+    // workspace: n members' key maps [n][padded] | uint8 map [padded]
+    rc = ensure_dsl(h, (size_t)(n * p0.padded * 4 + p0.padded));
+    if (rc) return rc;
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    uint32_t* keys = reinterpret_cast<uint32_t*>(h->d_dsl);
+    uint8_t* map = reinterpret_cast<uint8_t*>(keys + n * p0.padded);
+    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    for (int k = 0; k < n; ++k) {   // every member's key pass, into its own buffer
+        rc = dslice_keys(h, dslice_plan(P, num_disp, n, k), width, height, radius, guided, keys + k * p0.padded, s);
+        if (rc) return rc;
+    }
+    // the reduce-scatter's MIN (into member 0's buffer), then each member's chunk finalised into
+    // the all-gather's slot k
+    for (int k = 1; k < n; ++k)
+        SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(keys), reinterpret_cast<const int*>(keys + k * p0.padded),
+                                   p0.padded, s));
+    for (int k = 0; k < n; ++k) {
+        const DslicePlan p = dslice_plan(P, num_disp, n, k);
+        rc = dslice_finalise(keys + k * p.chunk, p.chunk, radius, guided, map + k * p.chunk, s);
+        if (rc) return rc;
+    }
+    SM_HIP(copy2d(disp_out, out_pitch, map, width, width, height, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    return SM_OK;
 }
 
 SM_API int sm_group_block_match_batch_u8(sm_group* g, const uint8_t* const* lefts, const uint8_t* const* rights,

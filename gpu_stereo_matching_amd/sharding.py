@@ -29,9 +29,25 @@ def frame_shard(n_frames: int, rank: int, world: int) -> List[int]:
     return list(range(lo, hi))
 
 
+def dslice_plan(pixels: int, num_disp: int, rank: int, world: int) -> Tuple[int, int, int, int]:
+    """(d_lo, d_hi, chunk, padded_pixels) of `rank`: the library's own plan (sm_dslice_plan), the
+    one sm_group_dslice_block_match_u8 uses, so the torch and C paths cannot drift apart.  Rank k
+    scans d in [k*D/G, (k+1)*D/G) (empty when G > D); the keys are padded to G*chunk pixels and the
+    reduce-scatter hands rank k pixels [k*chunk, (k+1)*chunk)."""
+    import ctypes
+    from . import _capi
+    lib = _capi.load()
+    lo, hi = ctypes.c_int(), ctypes.c_int()
+    chunk, padded = ctypes.c_int64(), ctypes.c_int64()
+    _capi.check(lib.sm_dslice_plan(pixels, num_disp, world, rank, ctypes.byref(lo), ctypes.byref(hi),
+                                   ctypes.byref(chunk), ctypes.byref(padded)))
+    return lo.value, hi.value, chunk.value, padded.value
+
+
 def dslice_bounds(num_disp: int, rank: int, world: int) -> Tuple[int, int]:
     """Disparity slice [lo, hi) of `rank`; empty slices are allowed when world > num_disp."""
-    return rank * num_disp // world, (rank + 1) * num_disp // world
+    lo, hi, _, _ = dslice_plan(1, num_disp, rank, world)
+    return lo, hi
 
 
 def seed_key(radius: int) -> int:
@@ -69,7 +85,7 @@ def keys_to_disparity_host(keys, radius: int):
 
 def padded_pixels(height: int, width: int, world: int) -> int:
     """Pixels rounded up to a multiple of the world size (the reduce-scatter chunking)."""
-    return -(-(height * width) // world) * world
+    return dslice_plan(height * width, 1, 0, world)[3]
 
 
 def dslice_buffers(height: int, width: int, world: int, device):

@@ -53,12 +53,18 @@ enum {
     SM_STAGED = 8u          /* box path through explicit HBM volumes (AD u8 -> SAD u16 -> WTA),
                                the reference's two-kernel data flow (Device.cu:19-64); same
                                output as the fused kernel, bandwidth-bound; not with
-                               SM_AGG_GUIDED or SM_LR_CHECK, radius <= 7 */
+                               SM_AGG_GUIDED or SM_LR_CHECK, radius <= 7.  Frames run in launch
+                               groups of up to 8 (SM_PARAM_STAGED_GROUP), and the handle keeps the
+                               volumes' workspace, 3*P*D (+ P with SM_MEDIAN) bytes per frame of a
+                               group, for its lifetime: ~6.4 GB at 1080p D=128 with 8-frame groups
+                               (capped at 8 GiB), ~0.8 GB with groups of 1 */
 };
 
 /* ---- scalar parameters (sm_set_param_f) ---- */
 enum {
-    SM_PARAM_GUIDED_EPS = 1 /* guided-filter epsilon in AD^2 units (default 6.5025 = 1e-4 * 255^2) */
+    SM_PARAM_GUIDED_EPS = 1,  /* guided-filter epsilon in AD^2 units (default 6.5025 = 1e-4 * 255^2) */
+    SM_PARAM_STAGED_GROUP = 2 /* SM_STAGED frames per launch group, 1..8 (default 8): bounds the
+                                 handle's staged workspace (see SM_STAGED) */
 };
 
 typedef struct sm_handle sm_handle;
@@ -279,10 +285,36 @@ SM_API int sm_group_block_match_batch_u8(sm_group *g, const uint8_t *const *left
  * aggregation; guided keys quantise q to 2^-14, so two fp32 costs closer than that may resolve
  * differently from a single pass.  flags: 0 (box) or SM_AGG_GUIDED.  Members must be distinct
  * devices; RCCL (librccl.so.1) is loaded on first use and one communicator per member is created
- * with ncclCommInitAll. */
+ * with ncclCommInitAll.
+ * Failure handling: the call runs in two phases.  Phase 1 (upload, slice keys, stream sync) runs on
+ * every member; if any member fails there, the call returns its error before any collective is
+ * enqueued.  In phase 2 (the collectives) a member that cannot take part aborts its communicator
+ * and the others, which poll their streams instead of blocking, abort theirs; the call returns the
+ * error and the next call re-creates the communicators.  Test hook: the environment variable
+ * SM_DSLICE_FAULT="<member>:keys" or "<member>:collective" injects a failure of that member in
+ * phase 1 or in place of its phase-2 collectives. */
 SM_API int sm_group_dslice_block_match_u8(sm_group *g, const uint8_t *left, const uint8_t *right, int width,
                                           int height, int pitch, int radius, int num_disp, unsigned flags,
                                           uint8_t *disp_out, int out_pitch);
+
+/* The d-slice plan shared by sm_group_dslice_block_match_u8 and the torch path (sharding.py): for a
+ * frame of `pixels` pixels split over `members`, member `member` scans d in [*d_lo, *d_hi) =
+ * [member*num_disp/members, (member+1)*num_disp/members) (empty when members > num_disp), the keys
+ * are padded to *padded_pixels = members * *chunk pixels with the "no match" key, and the MIN
+ * reduce-scatter hands the member pixels [member * *chunk, (member+1) * *chunk).  Host-only (no
+ * device, no handle); any output pointer may be NULL. */
+SM_API int sm_dslice_plan(int64_t pixels, int num_disp, int members, int member, int *d_lo, int *d_hi,
+                          int64_t *chunk, int64_t *padded_pixels);
+
+/* The d-slice split rehearsed on ONE device: the `members` members of sm_group_dslice_block_match_u8
+ * run one after another on this handle through the same per-member key pass, padding and
+ * finalisation; the RCCL MIN reduce-scatter is an elementwise MIN of their key maps and the
+ * all-gather puts chunk k at offset k*chunk.  The map must equal sm_block_match_u8's (box) for any
+ * member count; it lets the plan for n > 1 be checked on a one-GPU machine.  flags: 0 or
+ * SM_AGG_GUIDED; members 1..64.  Synchronous. */
+SM_API int sm_dslice_rehearse_u8(sm_handle *h, const uint8_t *left, const uint8_t *right, int width,
+                                 int height, int pitch, int radius, int num_disp, unsigned flags,
+                                 int members, uint8_t *disp_out, int out_pitch);
 
 #ifdef __cplusplus
 }

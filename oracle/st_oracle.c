@@ -400,7 +400,12 @@ ORA_API int ora_st_disp(const uint8_t *Lbgr, const uint8_t *Rbgr, int W, int H, 
 }
 
 /* GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180), pixel-major: the right view's cost at
- * (y, x, d) is the left view's at (y, x + d, d); where x + d >= W it repeats d - 1's */
+ * (y, x, d) is the left view's at (y, x + d, d); where x + d >= W it repeats d - 1's.
+ * W < D (max_level wider than the frame): the reference's second loop starts at x = w - maxLevel
+ * (StereoHelper.cpp:168), a negative column, so it writes into row y - 1 and, for y = 0, before the
+ * buffer: undefined behaviour with no defined output.  This port clamps the start to x = 0, the
+ * in-bounds reading (every pixel then takes the per-pixel rule above); results for W < D are
+ * therefore PARITY UNPINNED, a defined extension, not reference behaviour. */
 ORA_API void ora_st_right_cost(const float *left, int W, int H, int D, float *right)
 {
     memcpy(right, left, sizeof(float) * (size_t)W * H * D);

@@ -28,6 +28,32 @@ def test_example_builds():
     assert os.path.exists(EXE), "examples/build/single_frame missing: run __graft_entry__.build()"
 
 
+CVMAT_SRC = os.path.join(ROOT, "tests", "native", "cvmat_single_frame.cpp")
+CVMAT_EXE = os.path.join(ROOT, "examples", "build", "cvmat_single_frame")
+
+
+def test_cvmat_branch_compiles(tmp_path):
+    """stereo_bm.hpp's SM_WITH_OPENCV branch (blockMatching_gpu / testBM on cv::Mat, whose step is a
+    cv::MatStep) instantiates and links against libsm_hip.so.  OpenCV is absent: the test's own
+    minimal cv::Mat declares only the members the adapter touches (tests/native/cvmat_single_frame.cpp)."""
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
+                        CVMAT_SRC, "-o", str(tmp_path / "cvm"), "-L" + os.path.join(ROOT, "gpu_stereo_matching_amd"),
+                        "-lsm_hip"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_cvmat_single_frame_cpp(tmp_path, gray, bm_expected):
+    """singleFrame() (Caller.cpp:9-25) on the cv::Mat-shaped type, rows padded to 64 bytes: the golden
+    map of Caller.cpp:19's configuration, and testBM agrees with blockMatching_gpu."""
+    _write_pgm(tmp_path / "l.pgm", gray["Art_/view1"])
+    _write_pgm(tmp_path / "r.pgm", gray["Art_/view5"])
+    r = subprocess.run([CVMAT_EXE, str(tmp_path / "l.pgm"), str(tmp_path / "r.pgm"), str(tmp_path / "d.pgm"), "5",
+                        "64"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_read_pgm(tmp_path / "d.pgm"), bm_expected["Art_/r5/D64"])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pair,sad,rng", [("Art_", 5, 64), ("Books", 4, 64)])
 def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):

@@ -78,8 +78,9 @@ def test_group_error_from_a_member():
 @pytest.mark.parametrize("W,H,r,D", [(640, 333, 5, 128), (463, 370, 4, 64), (1920, 1080, 5, 256), (97, 31, 9, 37)])
 def test_group_dslice_one_member_box(single, W, H, r, D):
     """On the one GPU of the test box the RCCL communicator has one rank: the slice is the whole
-    range, the reduce-scatter and all-gather are the identity, and the map must equal the single
-    handle bit for bit (odd pixel counts exercise the chunk padding)."""
+    range, the reduce-scatter and all-gather are the identity (chunk == P, no padding), and the map
+    must equal the single handle bit for bit.  The n > 1 plan (slice bounds, padding, chunk order)
+    runs in test_dslice_rehearsal_* below."""
     import gpu_stereo_matching_amd as sm
     L, R = _pair(W, H, D)
     with sm.BlockMatcherGroup([0], 1920, 1080, 256) as g:
@@ -114,3 +115,48 @@ def test_group_dslice_rejects_repeated_device_and_flags():
         rc = g._lib.sm_group_dslice_block_match_u8(g._g, L.ctypes.data, R.ctypes.data, 64, 32, 64, 2, 16,
                                                    _capi.SM_LR_CHECK, out.ctypes.data, 64)
     assert rc == _capi.SM_ERR_INVALID_ARG
+
+
+# ---- the d-slice plan for n > 1 members on one device (sm_dslice_rehearse_u8) ---------------------
+@pytest.mark.parametrize("members", [2, 3, 5, 8])
+@pytest.mark.parametrize("W,H,r,D", [(97, 31, 4, 37), (463, 370, 4, 64), (41, 19, 2, 5), (1920, 1080, 5, 256)])
+def test_dslice_rehearsal_box_bit_exact(single, members, W, H, r, D):
+    """members > 1 through the same per-member key pass, seed padding (odd P) and chunk finalisation
+    as the RCCL group call; D = 5 with 8 members gives empty slices."""
+    L, R = _pair(W, H, D, seed=members)
+    assert np.array_equal(single.dslice_rehearse(L, R, r, D, members), single.match(L, R, r, D))
+
+
+@pytest.mark.parametrize("members", [2, 4, 7])
+def test_dslice_rehearsal_guided(single, members):
+    from oracle import oracle as O
+    W, H, r, D = 160, 90, 3, 48
+    L, R = _pair(W, H, D, seed=11)
+    got = single.dslice_rehearse(L, R, r, D, members, agg="guided")
+    want = single.match(L, R, r, D, agg="guided")
+    # keys quantise q to 2^-14 (DESIGN §9): equal except where two fp32 costs are that close, and
+    # every pixel of the combined map is within the tie tolerance of the fp64 oracle
+    assert (got == want).mean() >= 0.998
+    from guided_check import tie_aware_check
+    disp_o, q, best = O.guided_disp(L, R, r, D, EPS, want_q=True)
+    ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, D, W)
+    assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
+
+
+@pytest.mark.parametrize("phase", ["keys", "collective"])
+def test_dslice_member_failure_returns_error(single, monkeypatch, phase):
+    """A member failing before the collectives (keys) or in place of them (collective) makes the call
+    return its error instead of hanging the others; the next call re-creates what it must
+    and is bit-exact."""
+    import gpu_stereo_matching_amd as sm
+    from gpu_stereo_matching_amd import _capi
+    L, R = _pair(320, 97, 64, seed=5)
+    want = single.match(L, R, 4, 64)
+    with sm.BlockMatcherGroup([0], 512, 256, 64) as g:
+        assert np.array_equal(g.match_dslice(L, R, 4, 64), want)
+        monkeypatch.setenv("SM_DSLICE_FAULT", f"0:{phase}")
+        with pytest.raises(_capi.SMError) as e:
+            g.match_dslice(L, R, 4, 64)
+        assert e.value.code == _capi.SM_ERR_LAUNCH and "injected fault" in str(e.value)
+        monkeypatch.delenv("SM_DSLICE_FAULT")
+        assert np.array_equal(g.match_dslice(L, R, 4, 64), want)

@@ -569,6 +569,23 @@ def test_staged_launch_groups(matcher, oracle, torch, median):
     assert len(k) == 3 and all(t > 0 for t in k)
 
 
+def test_staged_group_param(oracle, torch):
+    """SM_PARAM_STAGED_GROUP bounds the staged workspace: groups of 1 and 3 give the same maps as 8;
+    values outside 1..8 (or not integers) are rejected."""
+    import gpu_stereo_matching_amd as sm
+    from gpu_stereo_matching_amd import _capi
+    pairs = [oracle.synth_pair(700 + b, 160, 48, 32) for b in range(5)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    with sm.BlockMatcher(0, 256, 64, 64) as m:
+        want = m.match_device(Lt, Rt, 3, 32)
+        for g in (1, 3, 8):
+            assert m._lib.sm_set_param_f(m._h, _capi.SM_PARAM_STAGED_GROUP, float(g)) == 0
+            assert torch.equal(m.match_device(Lt, Rt, 3, 32, agg="box-staged"), want)
+        for bad in (0.0, 9.0, 2.5):
+            assert m._lib.sm_set_param_f(m._h, _capi.SM_PARAM_STAGED_GROUP, bad) == _capi.SM_ERR_INVALID_ARG
+
+
 @pytest.mark.parametrize("seed", list(range(40)))
 def test_fuzz_box_lr_slices(matcher, oracle, torch, seed):
     """Seeded random shapes / radii / disparity counts / textures: box (host and batched device),
