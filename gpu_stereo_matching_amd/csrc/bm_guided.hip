@@ -104,21 +104,147 @@ struct GeoF {
     // each lane of a 32-lane group (the odd CS stride left 2-way conflicts, 25 % of LDS cycles)
     static constexpr int CSS_B = CSS0 + ((NSEG1 * SW1 - CSS0) % 32 + 32) % 32;
     static constexpr int CSS_OLD = CSS0 + 1;
+    static constexpr int MSA_ = AW % 4 == 2 ? AW : AW + ((6 - AW % 4) % 4);
     static constexpr int lds_for(int css) {
-        return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + TH * (AW | 1) * 8 +
+        return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + 2 * TH * MSA_ * 4 +
                AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
     }
     static constexpr int CSS = (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : 53248)) ? CSS_B : CSS_OLD;
-    // float2 per mm row: odd, so that S2H's ds_read_b64 of 32 rows (one per lane) tile all 64 banks
-    static constexpr int MS = AW | 1;
+    // mm is two float planes (sum a, sum b), rows of MSA floats.  S2V stores them lane-consecutively
+    // (ds_write_addtid_b32, 2 LDS cycles per 64 lanes against 6 for a float2 ds_write_b64); S2H reads
+    // its segment as ds_read_b64 pairs.  MSA = 2 (mod 4): the b64 reads of 32 lanes (32 rows, one
+    // segment; or, with the fused right view, rows {G, G+8, G+16, G+24} x 8 segments) fall on
+    // distinct bank pairs.
+    static constexpr int MSA = AW % 4 == 2 ? AW : AW + ((6 - AW % 4) % 4);
     static constexpr int ABS = NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW;   // float2 per a/b row
     static constexpr int RBW = 64 + kBandChunk;              // right band bytes per P row (one d-chunk)
     static constexpr int CS_BYTES = ((AHP * CSS * 4 > PHP * 64 ? AHP * CSS * 4 : PHP * 64) + 15) & ~15;  // lt aliases cs
-    static constexpr int MM_BYTES = TH * MS * 8;
+    static constexpr int MM_PLANE = TH * MSA * 4;            // bytes per mm plane
+    static constexpr int MM_BYTES = 2 * MM_PLANE;
     static constexpr int AB_BYTES = AH * ABS * 8;
     static constexpr int RB_BYTES = (PHP * RBW + 15) & ~15;
     static constexpr int LDS = CS_BYTES + MM_BYTES + AB_BYTES + RB_BYTES;
 };
+
+typedef float vf2 __attribute__((ext_vector_type(2)));   // a VGPR pair for asm operands
+
+// S2H's mm loads: N ds_read_b64 from plane A at `addr` and N from plane B at addr + PLANE, all in
+// flight before one s_waitcnt, written out in asm because the compiler pairs neighbouring b64 loads
+// into ds_read2_b64 (8 LDS cycles per pair against 2 per ds_read_b64, MI355X_MICROARCH.md LDS table).
+// The block waits for its own loads, so its outputs are ready when it ends.
+
+template <int N, int PLANE>
+__device__ __forceinline__ typename std::enable_if<N == 4>::type s2h_load_impl(uint32_t addr, vf2 (&a)[N], vf2 (&b)[N]) {
+    asm volatile("ds_read_b64 %0, %8 offset:0\n\t"
+                 "ds_read_b64 %1, %8 offset:8\n\t"
+                 "ds_read_b64 %2, %8 offset:16\n\t"
+                 "ds_read_b64 %3, %8 offset:24\n\t"
+                 "ds_read_b64 %4, %8 offset:%9\n\t"
+                 "ds_read_b64 %5, %8 offset:%10\n\t"
+                 "ds_read_b64 %6, %8 offset:%11\n\t"
+                 "ds_read_b64 %7, %8 offset:%12\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3])
+                 : "v"(addr), "i"(PLANE + 0), "i"(PLANE + 8), "i"(PLANE + 16), "i"(PLANE + 24)
+                 : "memory");
+}
+
+template <int N, int PLANE>
+__device__ __forceinline__ typename std::enable_if<N == 5>::type s2h_load_impl(uint32_t addr, vf2 (&a)[N], vf2 (&b)[N]) {
+    asm volatile("ds_read_b64 %0, %10 offset:0\n\t"
+                 "ds_read_b64 %1, %10 offset:8\n\t"
+                 "ds_read_b64 %2, %10 offset:16\n\t"
+                 "ds_read_b64 %3, %10 offset:24\n\t"
+                 "ds_read_b64 %4, %10 offset:32\n\t"
+                 "ds_read_b64 %5, %10 offset:%11\n\t"
+                 "ds_read_b64 %6, %10 offset:%12\n\t"
+                 "ds_read_b64 %7, %10 offset:%13\n\t"
+                 "ds_read_b64 %8, %10 offset:%14\n\t"
+                 "ds_read_b64 %9, %10 offset:%15\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4])
+                 : "v"(addr), "i"(PLANE + 0), "i"(PLANE + 8), "i"(PLANE + 16), "i"(PLANE + 24), "i"(PLANE + 32)
+                 : "memory");
+}
+
+template <int N, int PLANE>
+__device__ __forceinline__ typename std::enable_if<N == 6>::type s2h_load_impl(uint32_t addr, vf2 (&a)[N], vf2 (&b)[N]) {
+    asm volatile("ds_read_b64 %0, %12 offset:0\n\t"
+                 "ds_read_b64 %1, %12 offset:8\n\t"
+                 "ds_read_b64 %2, %12 offset:16\n\t"
+                 "ds_read_b64 %3, %12 offset:24\n\t"
+                 "ds_read_b64 %4, %12 offset:32\n\t"
+                 "ds_read_b64 %5, %12 offset:40\n\t"
+                 "ds_read_b64 %6, %12 offset:%13\n\t"
+                 "ds_read_b64 %7, %12 offset:%14\n\t"
+                 "ds_read_b64 %8, %12 offset:%15\n\t"
+                 "ds_read_b64 %9, %12 offset:%16\n\t"
+                 "ds_read_b64 %10, %12 offset:%17\n\t"
+                 "ds_read_b64 %11, %12 offset:%18\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5])
+                 : "v"(addr), "i"(PLANE + 0), "i"(PLANE + 8), "i"(PLANE + 16), "i"(PLANE + 24), "i"(PLANE + 32), "i"(PLANE + 40)
+                 : "memory");
+}
+
+template <int N, int PLANE>
+__device__ __forceinline__ typename std::enable_if<N == 7>::type s2h_load_impl(uint32_t addr, vf2 (&a)[N], vf2 (&b)[N]) {
+    asm volatile("ds_read_b64 %0, %14 offset:0\n\t"
+                 "ds_read_b64 %1, %14 offset:8\n\t"
+                 "ds_read_b64 %2, %14 offset:16\n\t"
+                 "ds_read_b64 %3, %14 offset:24\n\t"
+                 "ds_read_b64 %4, %14 offset:32\n\t"
+                 "ds_read_b64 %5, %14 offset:40\n\t"
+                 "ds_read_b64 %6, %14 offset:48\n\t"
+                 "ds_read_b64 %7, %14 offset:%15\n\t"
+                 "ds_read_b64 %8, %14 offset:%16\n\t"
+                 "ds_read_b64 %9, %14 offset:%17\n\t"
+                 "ds_read_b64 %10, %14 offset:%18\n\t"
+                 "ds_read_b64 %11, %14 offset:%19\n\t"
+                 "ds_read_b64 %12, %14 offset:%20\n\t"
+                 "ds_read_b64 %13, %14 offset:%21\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(a[6]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6])
+                 : "v"(addr), "i"(PLANE + 0), "i"(PLANE + 8), "i"(PLANE + 16), "i"(PLANE + 24), "i"(PLANE + 32), "i"(PLANE + 40), "i"(PLANE + 48)
+                 : "memory");
+}
+
+template <int N, int PLANE>
+__device__ __forceinline__ typename std::enable_if<N == 8>::type s2h_load_impl(uint32_t addr, vf2 (&a)[N], vf2 (&b)[N]) {
+    asm volatile("ds_read_b64 %0, %16 offset:0\n\t"
+                 "ds_read_b64 %1, %16 offset:8\n\t"
+                 "ds_read_b64 %2, %16 offset:16\n\t"
+                 "ds_read_b64 %3, %16 offset:24\n\t"
+                 "ds_read_b64 %4, %16 offset:32\n\t"
+                 "ds_read_b64 %5, %16 offset:40\n\t"
+                 "ds_read_b64 %6, %16 offset:48\n\t"
+                 "ds_read_b64 %7, %16 offset:56\n\t"
+                 "ds_read_b64 %8, %16 offset:%17\n\t"
+                 "ds_read_b64 %9, %16 offset:%18\n\t"
+                 "ds_read_b64 %10, %16 offset:%19\n\t"
+                 "ds_read_b64 %11, %16 offset:%20\n\t"
+                 "ds_read_b64 %12, %16 offset:%21\n\t"
+                 "ds_read_b64 %13, %16 offset:%22\n\t"
+                 "ds_read_b64 %14, %16 offset:%23\n\t"
+                 "ds_read_b64 %15, %16 offset:%24\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(a[6]), "=&v"(a[7]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6]), "=&v"(b[7])
+                 : "v"(addr), "i"(PLANE + 0), "i"(PLANE + 8), "i"(PLANE + 16), "i"(PLANE + 24), "i"(PLANE + 32), "i"(PLANE + 40), "i"(PLANE + 48), "i"(PLANE + 56)
+                 : "memory");
+}
+
+template <int N, int PLANE>
+__device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], float (&vb)[2 * N]) {
+    vf2 a[N], b[N];
+    s2h_load_impl<N, PLANE>(addr, a, b);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        va[2 * i] = a[i].x;
+        va[2 * i + 1] = a[i].y;
+        vb[2 * i] = b[i].x;
+        vb[2 * i + 1] = b[i].y;
+    }
+}
 
 // r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere; with the fused right
 // view r = 3 (7 outputs per S2H thread) spills at 168 and also runs at 2
@@ -139,7 +265,8 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
     uint8_t* lt = smem;                                                                 // [PHP][64] (aliases cs)
-    float2* mm = reinterpret_cast<float2*>(smem + G::CS_BYTES);                        // [TH][MS]
+    const float* mmA = reinterpret_cast<const float*>(smem + G::CS_BYTES);             // [TH][MSA] sum a
+    const float* mmB = reinterpret_cast<const float*>(smem + G::CS_BYTES + G::MM_PLANE); // [TH][MSA] sum b
     float2* abp = reinterpret_cast<float2*>(smem + G::CS_BYTES + G::MM_BYTES);         // [AH][ABS]
     uint8_t* rb = smem + G::CS_BYTES + G::MM_BYTES + G::AB_BYTES;                      // [PHP][RBW]
 
@@ -207,8 +334,14 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2).  Rows run across lanes
     // (measured 2 % faster than segments across lanes), except with the fused right view, whose
     // key chain runs from each segment to the next lane: lane = segment + 8 * row.
-    const int h2r = RIGHT ? (tid >> 3) : (tid & 31);
+    // With the right view, the 32-lane half-wave G = tid >> 5 holds rows {G, G + 8, G + 16, G + 24}
+    // (8 segments each) so that its b64 reads of the mm planes fall on distinct bank pairs.
+    const int h2r = RIGHT ? (((tid >> 3) & 3) * 8 + (tid >> 5)) : (tid & 31);
     const int h2s = RIGHT ? (tid & 7) : (tid >> 5);
+    // S2H's mm row segment (plane A) as an LDS byte address; plane B is MM_PLANE bytes further
+    const uint32_t h2off = (uint32_t)(G::CS_BYTES + (h2r * G::MSA + h2s * G::SW2) * 4);
+    // S2V's first mm row of this wave (plane A), for the add-TID stores
+    const uint32_t m0_mm = (uint32_t)(G::CS_BYTES + 8 * wave * G::MSA * 4);
     const int oy = y0 + h2r;
 
     // per-A-pixel constants (filled by the stats pass) and per-output WTA state.
@@ -371,7 +504,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         for (int r = 0; r < 8; ++r) {
             sa += v[r + 2 * R].x;
             sb += v[r + 2 * R].y;
-            mm[(8 * v2g + r) * G::MS + v2j] = make_float2(sa, sb);
+            // mmA / mmB [(8 v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32 (M0 = this
+            // wave's first mm row; the same s_nop hazard as S1V's stores)
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:%3\n\t"
+                         "ds_write_addtid_b32 %2 offset:%4"
+                         :
+                         : "s"(m0_mm), "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
+                         : "memory", "m0");
             sa -= v[r].x;
             sb -= v[r].y;
         }
@@ -380,19 +519,29 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // LIM: some output of the tile can have d > its dlim (tile-uniform; interior tiles skip the test)
     auto s2h = [&](int d, auto lim) {
         constexpr bool LIM = decltype(lim)::value;
-        const float2* row = mm + h2r * G::MS + h2s * G::SW2;
+        constexpr int NR = G::SW2 + 2 * R;   // mm values read per plane
+        float va[NR], vb[NR];
+        if constexpr (G::SW2 % 2 == 0) {
+            s2h_load<NR / 2, G::MM_PLANE>(h2off, va, vb);
+        } else {   // odd segment starts: 4-byte reads
+            const float* ra = mmA + h2r * G::MSA + h2s * G::SW2;
+            const float* rbb = mmB + h2r * G::MSA + h2s * G::SW2;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                va[k] = ra[k];
+                vb[k] = rbb[k];
+            }
+        }
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
-            const float2 v = row[k];
-            sa += v.x;
-            sb += v.y;
+            sa += va[k];
+            sb += vb[k];
         }
 #pragma unroll
         for (int o = 0; o < G::SW2; ++o) {
-            const float2 vin = row[o + 2 * R];
-            sa += vin.x;
-            sb += vin.y;
+            sa += va[o + 2 * R];
+            sb += vb[o + 2 * R];
             const float q = sa * oI[o] + sb;
             const bool take = (!LIM || d <= dlim[o]) && q < bq[o];
             bq[o] = take ? q : bq[o];
@@ -404,9 +553,8 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                 const int key = ((int)qs << 8) | (7 * G::SW2 + o);
                 rk[o] = key < rk[o] ? key : rk[o];
             }
-            const float2 vout = row[o];
-            sa -= vout.x;
-            sb -= vout.y;
+            sa -= va[o];
+            sb -= vb[o];
         }
         chain_step(d);
     };

@@ -15,7 +15,8 @@ struct StWorkspace {
     int* tree_i = nullptr;     // (5P + 2) per tree: rank, parent, first, child, level offsets
     uint8_t* tree_b = nullptr; // P per tree: distance to the parent
     float* table = nullptr;    // 256 per tree: exp(-i / (255 sigma))
-    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0;
+    int* task = nullptr;       // per tree: the wave filter's level tasks (int4 each), up to 2 * (P + levels)
+    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0;
     ~StWorkspace();
     void release();
 };

@@ -204,6 +204,158 @@ __global__ __launch_bounds__(kFT) void st_filter_kernel(FilterJobs jobs, int P) 
     }
 }
 
+// ---- the same filter, one wave per disparity (st_filter_wave_kernel) ----
+// A tree level's values depend only on the next (leaf to root) or the previous (root to leaf) level,
+// and in BFS order the children of one level are exactly the next level, contiguous.  So one wave per
+// disparity walks the levels with the two live levels in LDS (ping-pong buffers of the widest
+// level), wave-synchronous: no workgroup barrier and no global store -> load round trip per level,
+// which bound st_filter_kernel (~0.7 us per level).  The host cuts every level into tasks of <= 64
+// nodes (one node per lane): x = first node, y = count | (level parity << 8), z = the level's first
+// node, w = the first node of the level the task reads (children up, parents down).  Each lane's
+// global operands (cost / metadata) are loaded kStPre tasks ahead into a register ring, so the loads of
+// later levels are in flight while a level's LDS chain runs.
+constexpr int kStPre = 4;
+
+struct WaveJob {
+    float* C;                  // in: cost, out: leaf-to-root sums (read again by the root-to-leaf pass)
+    float* F;                  // out: filtered cost
+    const int* parent;
+    const uint8_t* pdist;
+    const int* first;
+    const uint32_t* child;
+    const int4* task;          // [n_up tasks, leaf to root][n_dn tasks, root to leaf]
+    int n_up, n_dn;
+    int maxw;                  // widest level (LDS buffer length)
+    const float* table;
+};
+struct WaveJobs {
+    WaveJob j[2];
+};
+
+__global__ __launch_bounds__(64) void st_filter_wave_kernel(WaveJobs jobs, int P) {
+#pragma clang fp contract(off)
+    const WaveJob& jb = jobs.j[blockIdx.y];
+    extern __shared__ float sbuf[];          // [256] table | [maxw] level buffer 0 | [maxw] level buffer 1
+    float* table = sbuf;
+    float* lvl = sbuf + 256;                 // level buffer of parity q at lvl + q * maxw
+    const int lane = threadIdx.x, maxw = jb.maxw;
+    for (int k = lane; k < 256; k += 64) table[k] = jb.table[k];
+    float* __restrict__ U = jb.C + (int64_t)blockIdx.x * P;
+    float* __restrict__ Fd = jb.F + (int64_t)blockIdx.x * P;
+    const int4* task = jb.task;
+    __syncthreads();
+
+    // Software pipeline over the tasks, kStPre deep: at task t the wave consumes the node operands
+    // loaded kStPre tasks earlier, issues those of task t + kStPre (its record arrived kStPre tasks
+    // ago) and the record of task t + 2 kStPre.  Every load is unconditional (indices clamped to a
+    // valid task / node), so the compiler's vmcnt waits count exactly the loads still needed.
+    // Records are vector loads of one uniform address; their fields stay in VGPRs.
+    // Records are loaded one dword per lane (lane & 3), so the compiler cannot take them for uniform
+    // values and move them into SGPRs as soon as they are loaded (which waits for the load); the fields
+    // are read out with v_readlane when the record is used, kStPre tasks after its load.
+    auto pass = [&](const int4* tk0, int nt, auto node_load, auto body) {
+        if (nt <= 0) return;
+        const int* tw = reinterpret_cast<const int*>(tk0) + (lane & 3);
+        auto rec_load = [&](int t) { return tw[4 * min(t, nt - 1)]; };
+        auto fields = [&](int v) {
+            return make_int4(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 1),
+                             __builtin_amdgcn_readlane(v, 2), __builtin_amdgcn_readlane(v, 3));
+        };
+        using NodeT = decltype(node_load(int4{}));
+        int rec[kStPre], nrec[kStPre];
+        NodeT nd[kStPre];
+#pragma unroll
+        for (int k = 0; k < kStPre; ++k) {
+            rec[k] = rec_load(k);
+            nd[k] = node_load(fields(rec[k]));
+            nrec[k] = rec_load(k + kStPre);
+        }
+        for (int t0 = 0; t0 < nt; t0 += kStPre) {
+#pragma unroll
+            for (int k = 0; k < kStPre; ++k) {
+                const int t = t0 + k;
+                if (t < nt) body(fields(rec[k]), nd[k]);
+                __builtin_amdgcn_wave_barrier();
+                rec[k] = nrec[k];
+                nd[k] = node_load(fields(rec[k]));
+                nrec[k] = rec_load(t + 2 * kStPre);
+            }
+        }
+    };
+    auto node_of = [&](const int4& r) { return r.x + min(lane, (r.y & 0xFF) - 1); };
+
+    // ---- leaf to root: u = C[i] + sum_z table[dist_z] * u(child z), children in order ----
+    struct UpNode {
+        float c;
+        uint32_t ch;
+        int f;
+    };
+    const uint32_t* __restrict__ child = jb.child;
+    const int* __restrict__ first = jb.first;
+    pass(task, jb.n_up,
+         [&](const int4& r) {
+             const int i = node_of(r);
+             return UpNode{U[i], child[i], first[i]};
+         },
+         [&](const int4& r, const UpNode& n0) {
+             const int cnt = r.y & 0xFF, q = (r.y >> 8) & 1;
+             if (lane < cnt) {
+                 const float* nxt = lvl + (q ^ 1) * maxw + (n0.f - r.w);
+                 const int n = (int)(n0.ch & 0xFFu);
+                 float u = n0.c;
+                 // at most 3 children (a grid node has 4 neighbours, one of them its parent; the root is
+                 // the corner pixel 0): all six LDS reads issued together, absent children's terms dropped
+                 // (their reads stay inside the level buffers)
+                 float cv[3], wv[3];
+#pragma unroll
+                 for (int z = 0; z < 3; ++z) {
+                     cv[z] = nxt[z < n ? z : 0];
+                     wv[z] = table[(n0.ch >> (8 * (z + 1))) & 0xFFu];
+                 }
+#pragma unroll
+                 for (int z = 0; z < 3; ++z) {
+                     const float tt = cv[z] * wv[z];
+                     u = z < n ? u + tt : u;
+                 }
+                 lvl[q * maxw + r.x + lane - r.z] = u;
+                 if (n) U[r.x + lane] = u;
+             }
+         });
+    __syncthreads();   // the U stores have completed (vmcnt) before the root-to-leaf pass reads them back
+
+    // ---- root to leaf: F[i] = w (F[parent] - w U[i]) + U[i] ----
+    const int* __restrict__ parent = jb.parent;
+    const uint8_t* __restrict__ pdist = jb.pdist;
+    if (lane == 0) {
+        const float u0 = __hip_atomic_load(&U[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        Fd[0] = u0;
+        lvl[0] = u0;   // level 0 (the root) has parity 0
+    }
+    __builtin_amdgcn_wave_barrier();
+    struct DnNode {
+        float u;
+        int p;
+        uint32_t dd;
+    };
+    pass(task + jb.n_up, jb.n_dn,
+         [&](const int4& r) {
+             const int i = node_of(r);
+             // written by this wave's leaf-to-root pass: read past the (non-coherent) L1
+             return DnNode{__hip_atomic_load(&U[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), parent[i],
+                           (uint32_t)pdist[i]};
+         },
+         [&](const int4& r, const DnNode& n0) {
+             const int cnt = r.y & 0xFF, q = (r.y >> 8) & 1;
+             if (lane < cnt) {
+                 const float w = table[n0.dd], u = n0.u;
+                 const float tt = w * u;
+                 const float fv = w * (lvl[(q ^ 1) * maxw + n0.p - r.w] - tt) + u;
+                 lvl[q * maxw + r.x + lane - r.z] = fv;
+                 Fd[r.x + lane] = fv;
+             }
+         });
+}
+
 // GetDisparity_WTA (StereoHelper.cpp:131-154): strict < from d = 0; times scale, saturated
 __global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F, const int* __restrict__ rank, int P,
                                                      int D, int scale, uint8_t* __restrict__ out) {
@@ -285,6 +437,50 @@ FilterJob filter_job(float* C, float* F, const DevTree& d) {
     return FilterJob{C, F, d.parent, d.pdist, d.first, d.child, d.lev, d.nlev, d.table};
 }
 
+// The wave filter's tasks of one tree (st_filter_wave_kernel): every level cut into runs of <= 64 nodes,
+// leaf to root, then root to leaf from level 1.  Returns the widest level.
+int wave_tasks(const HostTree& t, std::vector<int4>& out, int& n_up, int& n_dn) {
+    const int nlev = (int)t.lev.size() - 1;
+    out.clear();
+    int maxw = 1;
+    auto cut = [&](int l, int other) {
+        const int lo = t.lev[l], hi = t.lev[l + 1];
+        maxw = std::max(maxw, hi - lo);
+        for (int s0 = lo; s0 < hi; s0 += 64) out.push_back(make_int4(s0, std::min(64, hi - s0) | ((l & 1) << 8), lo, other));
+    };
+    for (int l = nlev - 1; l >= 0; --l) cut(l, l + 1 < nlev ? t.lev[l + 1] : t.lev[l]);
+    n_up = (int)out.size();
+    for (int l = 1; l < nlev; ++l) cut(l, t.lev[l - 1]);
+    n_dn = (int)out.size() - n_up;
+    return maxw;
+}
+
+constexpr int kWaveMaxLevel = 7936;   // (256 + 2 * 7936) floats = 64 KB of LDS; wider trees keep st_filter_kernel
+
+// Host task list `tv` of tree `d` into task slot k (`per` int4 each) of the workspace, which the caller
+// has grown for all its slots before the first upload; tv must stay alive until the copy has run.
+hipError_t upload_wave_job(StWorkspace& ws, int k, size_t per, const std::vector<int4>& tv, float* C, float* F,
+                           const DevTree& d, int n_up, int n_dn, int maxw, hipStream_t s, WaveJob& j) {
+    if (tv.size() > per || ws.task_n < per * 4 * (size_t)(k + 1)) return hipErrorInvalidValue;
+    int4* dst = reinterpret_cast<int4*>(ws.task) + per * (size_t)k;
+    const hipError_t e = hipMemcpyAsync(dst, tv.data(), tv.size() * sizeof(int4), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    j = WaveJob{C, F, d.parent, d.pdist, d.first, d.child, dst, n_up, n_dn, maxw, d.table};
+    return hipSuccess;
+}
+
+// One filter launch over 1 or 2 jobs: the wave filter when every level fits its LDS buffers, else the
+// workgroup-per-disparity filter.
+hipError_t launch_filter(const FilterJobs& fj, const WaveJobs& wj, int njobs, int maxw, int D, int P, hipStream_t s) {
+    if (maxw <= kWaveMaxLevel) {
+        hipLaunchKernelGGL(st_filter_wave_kernel, dim3((unsigned)D, (unsigned)njobs), dim3(64),
+                           (size_t)(256 + 2 * maxw) * sizeof(float), s, wj, P);
+    } else {
+        hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, (unsigned)njobs), dim3(kFT), 0, s, fj, P);
+    }
+    return hipGetLastError();
+}
+
 float ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -300,13 +496,15 @@ void StWorkspace::release() {
     (void)hipFree(tree_i);
     (void)hipFree(tree_b);
     (void)hipFree(table);
+    (void)hipFree(task);
+    task = nullptr;
     w8 = nullptr;
     grad = nullptr;
     vol = nullptr;
     tree_i = nullptr;
     tree_b = nullptr;
     table = nullptr;
-    w8_n = grad_n = vol_n = tree_i_n = tree_b_n = table_n = 0;
+    w8_n = grad_n = vol_n = tree_i_n = tree_b_n = table_n = task_n = 0;
 }
 
 #define ST_CHK(x)                          \
@@ -348,15 +546,20 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     const float tree_ms = ms_since(t0);
     DevTree dt = tree_slot(ws, P, 0);
     ST_CHK(upload_tree(t, table, P, dt, s));
+    std::vector<int4> tv;
+    int n_up = 0, n_dn = 0;
+    const int maxw = wave_tasks(t, tv, n_up, n_dn);
+    ST_CHK(grow(ws.task, ws.task_n, tv.size() * 4));
     float* C = ws.vol;
     float* F = ws.vol + (size_t)P * D;
+    WaveJobs wj{};
+    ST_CHK(upload_wave_job(ws, 0, tv.size(), tv, C, F, dt, n_up, n_dn, maxw, s, wj.j[0]));
     hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
                        dt.rank, D, C);
     ST_CHK(hipGetLastError());
     FilterJobs jobs{};
     jobs.j[0] = filter_job(C, F, dt);
-    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 1), dim3(kFT), 0, s, jobs, (int)P);
-    ST_CHK(hipGetLastError());
+    ST_CHK(launch_filter(jobs, wj, 1, maxw, D, (int)P, s));
     uint8_t* raw = ws.w8;   // the weights are consumed: reuse for the unfiltered map
     hipLaunchKernelGGL(st_wta_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, F, dt.rank, (int)P, D,
                        scale, raw);
@@ -442,7 +645,15 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     FilterJobs jobs{};
     jobs.j[0] = filter_job(C0, F0, d0);
     jobs.j[1] = filter_job(C1, F1, d1);
-    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 2), dim3(kFT), 0, s, jobs, (int)P);
+    std::vector<int4> tv0, tv1;
+    int nu0 = 0, nd0 = 0, nu1 = 0, nd1 = 0;
+    const int mw0 = wave_tasks(tl, tv0, nu0, nd0), mw1 = wave_tasks(tr, tv1, nu1, nd1);
+    const size_t per = std::max(tv0.size(), tv1.size());
+    ST_CHK(grow(ws.task, ws.task_n, per * 4 * 2));
+    WaveJobs wj{};
+    ST_CHK(upload_wave_job(ws, 0, per, tv0, C0, F0, d0, nu0, nd0, mw0, s, wj.j[0]));
+    ST_CHK(upload_wave_job(ws, 1, per, tv1, C1, F1, d1, nu1, nd1, mw1, s, wj.j[1]));
+    ST_CHK(launch_filter(jobs, wj, 2, std::max(mw0, mw1), D, (int)P, s));
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, 1, raw0);
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F1, d1.rank, (int)P, D, 1, raw1);
     ST_CHK(hipGetLastError());
@@ -471,7 +682,13 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(hipGetLastError());
     FilterJobs job2{};
     job2.j[0] = filter_job(C0, F0, d0);
-    hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, 1), dim3(kFT), 0, s, job2, (int)P);
+    std::vector<int4> tv2;
+    int nu2 = 0, nd2 = 0;
+    const int mw2 = wave_tasks(td, tv2, nu2, nd2);
+    ST_CHK(grow(ws.task, ws.task_n, tv2.size() * 4));   // the first run's uploads completed at the sync above
+    WaveJobs wj2{};
+    ST_CHK(upload_wave_job(ws, 0, tv2.size(), tv2, C0, F0, d0, nu2, nd2, mw2, s, wj2.j[0]));
+    ST_CHK(launch_filter(job2, wj2, 1, mw2, D, (int)P, s));
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, scale, raw0);
     ST_CHK(hipGetLastError());
     ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, d_out, W, P, s));
