@@ -310,6 +310,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     for (int k = 0; k < G::NV; ++k) mul[k] = (uint32_t)lt[(a0 + k) * 64 + c] | kPOne;
     __syncthreads();   // lt (aliased with cs) is consumed
 
+    // S1H's constants as SGPR operands: the compiler would fold them into literal operands, whose 64-bit
+    // encodings issue slower than the 32-bit VOP2 form with an SGPR source (38 ands, 9 ors and 9 adds
+    // per wave and d)
+    uint32_t k_plow = kPLow, k_magic = 0x4B000000u;
+    float k_magicf = -8388608.0f;
+    asm volatile("" : "+s"(k_plow), "+s"(k_magic), "+s"(k_magicf));
     // S1H ownership: A row h1i, segment h1s (threads >= AH*NSEG1 idle in S1H)
     const bool h1_on = tid < G::AH * G::NSEG1;
     const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
@@ -397,6 +403,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) rv[k] = STATS ? 0u : (uint32_t)rc[(a0 + k) * G::RBW];
         uint32_t T = 0u, Tp[2 * R + 1];
+        // M0 = this wave's first cs row for the add-TID stores below, set once per call.  An SALU write of
+        // M0 needs one wait state before an add-TID LDS instruction reads it (the compiler does not see
+        // the hazard inside the asm): s_nop 0.  Nothing else in this kernel uses M0 (checked in the
+        // ISA), and volatile asm statements keep their order, so every store below sees this value.
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(m0_cs) : "m0");
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) {
             const uint32_t ad = __builtin_amdgcn_sad_u8(mul[k], rv[k], 0xFFFFFFF0u);
@@ -405,13 +416,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                 const uint32_t old = (k == 2 * R) ? 0u : Tp[(k - 2 * R - 1) % (2 * R + 1)];
                 const uint32_t val = m ? T - old : 0u;
                 // cs[(a0 + k - 2R) * CSS + lane]: lane-consecutive dwords, so ds_write_addtid_b32
-                // (M0 = this wave's first cs row; 2 LDS cycles per store instead of 4).  An SALU write
-                // of M0 needs one wait state before an add-TID LDS instruction reads it (the compiler
-                // does not see the hazard inside the asm): s_nop 0.
-                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:%2"
-                             :
-                             : "s"(m0_cs), "v"(val), "i"((k - 2 * R) * G::CSS * 4)
-                             : "memory", "m0");
+                // (2 LDS cycles per store instead of 4)
+                asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(val), "i"((k - 2 * R) * G::CSS * 4)
+                             : "memory");
             }
             Tp[k % (2 * R + 1)] = T;
         }
@@ -425,13 +432,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         for (int k = 0; k < 2 * R; ++k) {
             const uint32_t v = row[k];
             sp += v >> 20;
-            sip += v & kPLow;
+            sip += v & k_plow;
         }
 #pragma unroll
         for (int o = 0; o < G::SW1; ++o) {
             const uint32_t vin = row[o + 2 * R];
             sp += vin >> 20;
-            sip += vin & kPLow;
+            sip += vin & k_plow;
             // guide statistics: sp = SI, sip = SII
             const int j = h1s * G::SW1 + o;                         // A column
             const int x = x0 - R + j;
@@ -445,7 +452,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             invN[o] = inimg ? 1.0f / (float)N : 0.f;
             const uint32_t vout = row[o];
             sp -= vout >> 20;
-            sip -= vout & kPLow;
+            sip -= vout & k_plow;
         }
     };
     auto s1h = [&]() {
@@ -460,12 +467,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
             sp += v[k] >> 20;
-            sip += v[k] & kPLow;
+            sip += v[k] & k_plow;
         }
 #pragma unroll
         for (int o = 0; o < G::SW1; ++o) {
             sp += v[o + 2 * R] >> 20;
-            sip += v[o + 2 * R] & kPLow;
+            sip += v[o + 2 * R] & k_plow;
             // N*SIp - SI*Sp = N^2 cov(I, p), |.| < 2^30, exactly: every factor fits a signed 24-bit
             // operand (SIp <= 121 * 255^2 < 2^23), so v_mul_i32_i24 + v_mad_i32_i24 (written out: the
             // compiler otherwise turns one product into a quarter-rate v_mul_lo_u32)
@@ -474,7 +481,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             asm("v_mad_i32_i24 %0, %1, %2, %0" : "+v"(num) : "v"(nN[o]), "v"(sip));
             const float a = (float)num * invden[o];
             // float(Sp) without v_cvt (a quarter-rate op here): Sp < 2^22, float(2^23 + Sp) is exact
-            const float fsp = __builtin_bit_cast(float, 0x4B000000u | sp) - 8388608.0f;
+            const float fsp = __builtin_bit_cast(float, k_magic | sp) + k_magicf;
             const float b = __builtin_fmaf(-a, fSI[o], fsp) * invN[o];
             // one ds_write_b64 (the compiler emits ds_write2_b32 for a float2 store here)
             asm volatile("ds_write_b64 %0, %1 offset:%2"
@@ -482,7 +489,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                          : "v"(h1off), "v"(__builtin_bit_cast(double, make_float2(a, b))), "i"(8 * o)
                          : "memory");
             sp -= v[o] >> 20;
-            sip -= v[o] & kPLow;
+            sip -= v[o] & k_plow;
         }
     };
     // ================= S2V =================
@@ -500,17 +507,17 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             sa += v[k].x;
             sb += v[k].y;
         }
+        // M0 = this wave's first mm row (plane A), set once per call as in S1V
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(m0_mm) : "m0");
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             sa += v[r + 2 * R].x;
             sb += v[r + 2 * R].y;
-            // mmA / mmB [(8 v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32 (M0 = this
-            // wave's first mm row; the same s_nop hazard as S1V's stores)
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:%3\n\t"
-                         "ds_write_addtid_b32 %2 offset:%4"
+            // mmA / mmB [(8 v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32
+            asm volatile("ds_write_addtid_b32 %0 offset:%2\n\tds_write_addtid_b32 %1 offset:%3"
                          :
-                         : "s"(m0_mm), "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
-                         : "memory", "m0");
+                         : "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
+                         : "memory");
             sa -= v[r].x;
             sb -= v[r].y;
         }

@@ -19,6 +19,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -349,6 +350,49 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
     return rc;
 }
 
+// Page-locked blocks from sm_host_alloc: a map the caller receives into one of them is written by the
+// kernel straight over PCIe (zero-copy), with no separate device-to-host copy.
+std::mutex g_host_mu;
+std::map<uintptr_t, size_t> g_host_blocks;
+
+void host_blocks_add(void* p, size_t n) {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_blocks[(uintptr_t)p] = n;
+}
+
+void host_blocks_remove(void* p) {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_blocks.erase((uintptr_t)p);
+}
+
+// Device address of [p, p + bytes) when that range lies in one sm_host_alloc block, else nullptr.
+uint8_t* host_block_device_ptr(void* p, size_t bytes) {
+    uintptr_t base = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_blocks.upper_bound((uintptr_t)p);
+        if (it == g_host_blocks.begin()) return nullptr;
+        --it;
+        if ((uintptr_t)p + bytes > it->first + it->second) return nullptr;
+        base = it->first;
+    }
+    void* dbase = nullptr;
+    if (hipHostGetDevicePointer(&dbase, reinterpret_cast<void*>(base), 0) != hipSuccess || !dbase) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(dbase) + ((uintptr_t)p - base);
+}
+
+// SM_ZERO_COPY=0 keeps the device buffer + download for every call (A/B timing)
+bool zero_copy_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SM_ZERO_COPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Host-pointer pass over one frame (or one row band of a frame: sm_group_*).  Only result rows
 // [keep0, keep1) are downloaded, into disp_out / right_out / mask_out pointing at row keep0.
 int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
@@ -387,17 +431,23 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
         }
         aux = h->d_aux;
     }
+    // zero-copy map: a whole-frame call whose map goes to an sm_host_alloc block and is only written by
+    // the last kernel (no LR check, which reads the left map back)
+    uint8_t* mapped = nullptr;
+    if (zero_copy_enabled() && keep0 == 0 && keep1 == height && !right_out && !mask_out && !(flags & SM_LR_CHECK))
+        mapped = host_block_device_ptr(disp_out, (size_t)(height - 1) * out_pitch + width);
     SM_HIP(hipEventRecord(h->ev[0], s));
     SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     SM_HIP(hipEventRecord(h->ev[1], s));
-    rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
-                    right_out ? aux : nullptr, mask_out ? aux + P : nullptr, width, P, s);
+    rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags,
+                    mapped ? mapped : h->d_disp, mapped ? out_pitch : width, P, right_out ? aux : nullptr,
+                    mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
     SM_HIP(hipEventRecord(h->ev[2], s));
     const int64_t k0 = (int64_t)keep0 * width;
     const int nk = keep1 - keep0;
-    SM_HIP(copy2d(disp_out, out_pitch, h->d_disp + k0, width, width, nk, hipMemcpyDeviceToHost, s));
+    if (!mapped) SM_HIP(copy2d(disp_out, out_pitch, h->d_disp + k0, width, width, nk, hipMemcpyDeviceToHost, s));
     if (right_out) SM_HIP(copy2d(right_out, out_pitch, aux + k0, width, width, nk, hipMemcpyDeviceToHost, s));
     if (mask_out) SM_HIP(copy2d(mask_out, out_pitch, aux + P + k0, width, width, nk, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
@@ -852,13 +902,16 @@ SM_API int sm_host_alloc(size_t bytes, void** out) {
     if (!out) return fail(SM_ERR_INVALID_ARG, "null out pointer");
     *out = nullptr;
     if (bytes == 0) return fail(SM_ERR_INVALID_ARG, "zero-byte host allocation");
-    // portable: usable by every device's handle (a group's members copy from one frame)
-    SM_HIP(hipHostMalloc(out, bytes, hipHostMallocPortable));
+    // portable: usable by every device's handle (a group's members copy from one frame); mapped: the
+    // kernels may write a map straight into it (host_match_rows)
+    SM_HIP(hipHostMalloc(out, bytes, hipHostMallocPortable | hipHostMallocMapped));
+    host_blocks_add(*out, bytes);
     return SM_OK;
 }
 
 SM_API int sm_host_free(void* p) {
     if (!p) return SM_OK;
+    host_blocks_remove(p);
     SM_HIP(hipHostFree(p));
     return SM_OK;
 }

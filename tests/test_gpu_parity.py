@@ -631,6 +631,33 @@ def test_pinned_host_buffers(sm, matcher, oracle):
     assert np.array_equal(chk, chk_o) and np.array_equal(rd, rd_o) and np.array_equal(mask, mask_o)
 
 
+@pytest.mark.parametrize("agg,med", [("box", False), ("box", True), ("guided", False), ("box-staged", False),
+                                     ("box-staged", True)])
+def test_zero_copy_map(sm, matcher, oracle, agg, med):
+    """A map received into an sm_host_alloc block is written by the last kernel straight into it
+    (zero-copy, no download): same map as a pageable output, for each kernel that can write it last;
+    the block is refilled with garbage between calls so a missed write shows.  A pitched map inside a
+    larger block (raw C ABI, out_pitch > width) too."""
+    import ctypes
+    from gpu_stereo_matching_amd import _capi
+    W, H, D, r = 517, 203, 64, 4
+    L, R = oracle.synth_pair(77, W, H, D)
+    want = matcher.match(L, R, r, D, agg=agg, median=med)
+    Op = sm.host_empty((H, W))
+    for fill in (0, 255, 0x5A):
+        Op[...] = fill
+        assert np.array_equal(matcher.match(L, R, r, D, agg=agg, median=med, out=Op), want)
+    P2 = W + 37
+    big = sm.host_empty((H + 2, P2))
+    big[...] = 0xEE
+    view = big[1:, :]   # rows 1.. of the block, pitch P2
+    rc = matcher._lib.sm_block_match_u8(matcher._h, L.ctypes.data, R.ctypes.data, W, H, W, r, D,
+                                         sm._flags(agg, False, med), view.ctypes.data, P2)
+    assert rc == _capi.SM_OK
+    assert np.array_equal(big[1:H + 1, :W], want)
+    assert (big[0] == 0xEE).all() and (big[1:H + 1, W:] == 0xEE).all()   # nothing outside the map
+
+
 @pytest.mark.parametrize("W,H,D,r", [(333, 257, 64, 7), (640, 256, 96, 0), (500, 300, 128, 11),
                                      (1001, 400, 256, 15), (320, 260, 32, 3)])
 def test_pinned_odd_shapes(sm, matcher, oracle, W, H, D, r):

@@ -1,0 +1,38 @@
+"""Drop-in host round trip (sm_block_match_u8, 1080p D=128 r=5) on sm_host_alloc frames and map, with and
+without the zero-copy map (SM_ZERO_COPY=0 keeps the download).  Each setting runs in its own process,
+alternated 3 times; prints the median wall ms per call of each run and the last call's stage split."""
+import os, subprocess, sys, statistics
+if len(sys.argv) > 1 and sys.argv[1] == "child":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import time
+    import numpy as np
+    import gpu_stereo_matching_amd as sm
+    W, H, D, r = 1920, 1080, 128, 5
+    L, R = sm.synth_pair(1234, W, H, D)
+    with sm.BlockMatcher(0, W, H, 256) as m:
+        Lp, Rp, Op = sm.host_empty((H, W)), sm.host_empty((H, W)), sm.host_empty((H, W))
+        Lp[...] = L
+        Rp[...] = R
+        for _ in range(20):
+            m.match(Lp, Rp, r, D, out=Op)
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            m.match(Lp, Rp, r, D, out=Op)
+            ts.append(time.perf_counter() - t0)
+        print("RESULT", statistics.median(ts) * 1e3, *m.stage_ms())
+    sys.exit(0)
+res = {"1": [], "0": []}
+for _ in range(3):
+    for zc in ("1", "0"):
+        out = subprocess.run([sys.executable, __file__, "child"], env=dict(os.environ, SM_ZERO_COPY=zc),
+                             capture_output=True, text=True, timeout=200)
+        line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
+        if not line:
+            print(out.stdout, out.stderr)
+            sys.exit(1)
+        res[zc].append([float(v) for v in line[0].split()[1:]])
+for zc, name in (("0", "download (SM_ZERO_COPY=0)"), ("1", "zero-copy map")):
+    walls = [v[0] for v in res[zc]]
+    print(f"{name:28s} wall ms/call median {statistics.median(walls):.4f} all {[round(w, 4) for w in walls]} "
+          f"last stages upload/match/download {[round(x, 4) for x in res[zc][-1][1:]]}")
