@@ -214,7 +214,10 @@ __global__ __launch_bounds__(kFT) void st_filter_kernel(FilterJobs jobs, int P) 
 // node, w = the first node of the level the task reads (children up, parents down).  Each lane's
 // global operands (cost / metadata) are loaded kStPre tasks ahead into a register ring, so the loads of
 // later levels are in flight while a level's LDS chain runs.
-constexpr int kStPre = 4;
+#ifndef SM_ST_PRE
+#define SM_ST_PRE 4
+#endif
+constexpr int kStPre = SM_ST_PRE;
 
 struct WaveJob {
     float* C;                  // in: cost, out: leaf-to-root sums (read again by the root-to-leaf pass)

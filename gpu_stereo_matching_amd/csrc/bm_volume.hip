@@ -25,7 +25,6 @@ constexpr int kVT = 256;
 #ifndef SM_ADV_NT
 #define SM_ADV_NT 1
 #endif
-constexpr int kVPad = 16;   // zero bytes in front of the staged R row (x - d down to -15)
 
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -41,18 +40,29 @@ __device__ __forceinline__ uint32_t absdiff_u8x4(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, de) | (__builtin_bit_cast(uint32_t, dO) << 8);
 }
 
+
+// SEG output bytes per thread and d (16 or 64).  With 64 each lane stores its 64-B piece of the plane row
+// as four 16-B stores (lane l at 64 l + 16 k in store k): the pattern that measured 6.0 TB/s of pure
+// writes on this part against 5.5-5.8 for one lane-consecutive 16-B store per lane
+// (profiles/microbench/r02_hbm_vendor_ceilings.txt, "chunk 4/lane").
+#ifndef SM_ADV_SEG
+#define SM_ADV_SEG 16
+#endif
+template <int SEG>
 __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                         int W, int H, int pitch, int64_t fstride, int D,
                                                         uint8_t* __restrict__ dif, int64_t dstride) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [kVPad + W + 16]
+    constexpr int NQ = SEG / 4;                                      // dwords per thread and d
+    constexpr int kVPad = SEG;   // zero bytes in front of the staged R row (x - d down to -SEG)
+    extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [kVPad + nseg * SEG + 4]
     const int y = blockIdx.x, f = blockIdx.y;
     const int dc = (D + gridDim.z - 1) / gridDim.z;               // disparities of this block
     const int d_begin = blockIdx.z * dc, d_end = d_begin + dc < D ? d_begin + dc : D;
     const uint8_t* lr = L + (int64_t)f * fstride + (int64_t)y * pitch;
     const uint8_t* rr = R + (int64_t)f * fstride + (int64_t)y * pitch;
-    const int nseg = (W + 15) >> 4;
-    // stage the R row as dwords: rrow dword j = R bytes 4j - 16 .. 4j - 13 (0 outside the row)
-    for (int j = threadIdx.x; j < (kVPad + nseg * 16 + 4) / 4; j += kVT) {
+    const int nseg = (W + SEG - 1) / SEG;
+    // stage the R row as dwords: rrow dword j = R bytes 4j - kVPad .. 4j - kVPad + 3 (0 outside the row)
+    for (int j = threadIdx.x; j < (kVPad + nseg * SEG + 4) / 4; j += kVT) {
         const int c = 4 * j - kVPad;
         uint32_t v = 0;
         if (c >= 0 && c + 3 < W) {
@@ -62,7 +72,9 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
             for (int b = 0; b < 4; ++b)
                 if (c + b >= 0 && c + b < W) v |= (uint32_t)rr[c + b] << (8 * b);
         }
-        reinterpret_cast<uint32_t*>(rrow)[j] = v;
+        // SEG = 64: one pad dword after every 16 (64 B), so the 64-B-strided windows of consecutive
+        // lanes start on banks 17 apart instead of 16 (16-way conflicts without it)
+        reinterpret_cast<uint32_t*>(rrow)[SEG == 64 ? j + (j >> 4) : j] = v;
     }
     __syncthreads();
     const int64_t P = (int64_t)W * H;
@@ -73,13 +85,13 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     const int groups = kVT / nseg > 0 ? kVT / nseg : 1;
     const int seg = threadIdx.x % nseg, g = threadIdx.x / nseg;
     if (g >= groups) return;
-    const int x0 = seg * 16;
-    uint32_t l[4];
-    if (x0 + 16 <= W) {
-        __builtin_memcpy(l, lr + x0, 16);
+    const int x0 = seg * SEG;
+    uint32_t l[NQ];
+    if (x0 + SEG <= W) {
+        __builtin_memcpy(l, lr + x0, SEG);
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NQ; ++q) {
             uint32_t v = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -91,26 +103,38 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     }
 #pragma unroll 2
     for (int d = d_begin + g; d < d_end; d += groups) {
-        // R bytes at x0-d .. x0-d+15, from the padded row (index kVPad + x0 - d >= 0 while d <= x0 + 16)
-        uint32_t r[4];
+        // R bytes at x0-d .. x0-d+SEG-1, from the padded row (index kVPad + x0 - d >= 0 while d <= x0 + SEG; a
+        // larger d leaves every byte of the segment at x < d)
+        uint32_t r[NQ];
         const int start = kVPad + x0 - d;
         if (start >= 0) {
             const int base = start & ~3, sh = start & 3;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(rrow + base);
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-            r[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            r[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            r[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            r[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+            uint32_t wv[NQ + 1];
+            if constexpr (SEG == 64) {
+                // logical dword j0 + q lives at j0 + q + (j0 + q) / 16; with x0 a multiple of 64 the
+                // window's first dword j0 = 16 * seg + s (s uniform), so the pad before dword q is
+                // crossed at the same q in every lane
+                const int j0 = base >> 2, s16 = j0 & 15;
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(rrow) + j0 + (j0 >> 4);
+#pragma unroll
+                for (int q = 0; q <= NQ; ++q) wv[q] = w[q + (q + s16 >= 16 ? 1 : 0) + (q + s16 >= 32 ? 1 : 0)];
+            } else {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(rrow + base);
+#pragma unroll
+                for (int q = 0; q <= NQ; ++q) wv[q] = w[q];
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) r[q] = __builtin_amdgcn_alignbyte(wv[q + 1], wv[q], sh);
         } else {
-            r[0] = r[1] = r[2] = r[3] = 0u;   // every byte of this segment has x < d: masked below
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) r[q] = 0u;   // every byte of this segment has x < d: masked below
         }
-        uint32_t o[4];
+        uint32_t o[NQ];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = absdiff_u8x4(l[q], r[q]);
-        if (x0 < d + 16) {   // bytes with x < d are 0 (Device.cu:27-31 + the memset)
+        for (int q = 0; q < NQ; ++q) o[q] = absdiff_u8x4(l[q], r[q]);
+        if (x0 < d + SEG) {   // bytes with x < d are 0 (Device.cu:27-31 + the memset)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < NQ; ++q) {
                 uint32_t keep = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b) keep |= (x0 + 4 * q + b >= d ? 0xFFu : 0u) << (8 * b);
@@ -118,13 +142,16 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
             }
         }
         uint8_t* dst = out + (int64_t)d * P + x0;
-        if (vec) {
+        if (vec && x0 + SEG <= W) {
             // streaming output (P*D bytes, larger than the MALL): nontemporal 16-B stores
-            const u32x4 v = {o[0], o[1], o[2], o[3]};
-            if (SM_ADV_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
-            else *reinterpret_cast<u32x4*>(dst) = v;
+#pragma unroll
+            for (int k = 0; k < NQ / 4; ++k) {
+                const u32x4 v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                if (SM_ADV_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst) + k);
+                else reinterpret_cast<u32x4*>(dst)[k] = v;
+            }
         } else {
-            const int n = W - x0 < 16 ? W - x0 : 16;
+            const int n = W - x0 < SEG ? W - x0 : SEG;
             for (int b = 0; b < n; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
         }
     }
@@ -134,14 +161,15 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
 
 hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int64_t fstride, int batch,
                             int D, uint8_t* dif, int64_t dstride, hipStream_t s) {
-    const int nseg = (W + 15) / 16;
+    constexpr int SEG = SM_ADV_SEG;
+    const int nseg = (W + SEG - 1) / SEG;
     if (W <= 0 || H <= 0 || D <= 0 || batch <= 0 || nseg > kVT) return hipErrorInvalidValue;
-    const size_t lds = (size_t)(kVPad + nseg * 16 + 4 + 15) & ~(size_t)15;
+    const size_t lds = ((size_t)(SEG + nseg * SEG + 4) * (SEG == 64 ? 17 : 16) / 16 + 4 + 15) & ~(size_t)15;
     // enough blocks in flight (>= ~4 per CU of 256) to keep the stores streaming
     int dsplit = (SM_ADV_BLOCKS + H * batch - 1) / (H * batch);
     dsplit = dsplit < 1 ? 1 : (dsplit > D ? D : (dsplit > SM_ADV_MAXSPLIT ? SM_ADV_MAXSPLIT : dsplit));
-    hipLaunchKernelGGL(ad_volume_kernel, dim3(H, batch, dsplit), dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D,
-                       dif, dstride);
+    hipLaunchKernelGGL(ad_volume_kernel<SEG>, dim3(H, batch, dsplit), dim3(kVT), lds, s, L, R, W, H, pitch, fstride,
+                       D, dif, dstride);
     return hipGetLastError();
 }
 
