@@ -79,17 +79,31 @@ constexpr int kBandChunk = 32;
 constexpr uint32_t kPOne = 1u << 20;   // S1V multiplier L | 2^20: low 20 bits sum I*p, high 12 bits sum p
 constexpr uint32_t kPLow = kPOne - 1;
 
-template <int R>
+// Phase-1 wave roles (round 3): S1V on 2 waves over half the A rows each and S2V on the other 2 over
+// 16 output rows each, instead of both stages on all 4 waves over a quarter: S1V's integer running sums
+// re-walk their 2R-row warm-up once per wave, so two taller strips walk 62 P rows instead of 84, and
+// S2V reads each a/b row once per 16-row strip (52 reads instead of 72; its float sums still restart
+// every 8 rows, so the maps do not change).  Roles rotate with the workgroup index, so the
+// co-resident workgroups of a CU put their S1V waves on different SIMDs.
+#ifndef SM_G_ROLES
+#define SM_G_ROLES 1
+#endif
+constexpr bool kGuidedRoles = SM_G_ROLES != 0;
+
+template <int R, bool ROLES = kGuidedRoles>
 struct GeoF {
     static constexpr int TW = 64 - 4 * R;
     static constexpr int TH = 32;
     static constexpr int AW = TW + 2 * R;
     static constexpr int AH = TH + 2 * R;
     static constexpr int PH = TH + 4 * R;
-    static constexpr int RPW = (AH + 3) / 4;                 // A rows per wave in S1V
+    // phase 1 runs S1V on SV waves and S2V on the other 4 - SV (kGuidedRoles), else both on all 4
+    static constexpr int SV = ROLES ? 2 : 4;
+    static constexpr int RPS = TH / (ROLES ? 4 - SV : 4);     // output rows per S2V wave
+    static constexpr int RPW = (AH + SV - 1) / SV;           // A rows per wave in S1V
     static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
-    static constexpr int AHP = 4 * RPW;                      // cs rows incl. the last wave's pad rows
-    static constexpr int PHP = 4 * RPW + 2 * R;              // staged P rows incl. pad rows (>= PH)
+    static constexpr int AHP = SV * RPW;                     // cs rows incl. the last wave's pad rows
+    static constexpr int PHP = SV * RPW + 2 * R;             // staged P rows incl. pad rows (>= PH)
     static constexpr int NSEG1 = kT / AH;                    // S1H segments per A row
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
@@ -261,7 +275,10 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
-    using G = GeoF<R>;
+    // wave roles without the fused right view only: its key chain leaves no registers for the taller
+    // strips (168-VGPR budget, spills measured in the ISA)
+    constexpr bool ROLES = kGuidedRoles && !RIGHT;
+    using G = GeoF<R, ROLES>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
     uint8_t* lt = smem;                                                                 // [PHP][64] (aliases cs)
@@ -296,10 +313,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = ld4(L, py0 + i, px0 + 4 * j, W, H, pitch);
     }
     __syncthreads();
+    // phase-1 role of this wave: S1V strip `role` (role < SV) or S2V strip role - SV
+    const int role = ROLES ? __builtin_amdgcn_readfirstlane((wave + (int)blockIdx.x) & 3) : wave;
+    const bool is_s1v = !ROLES || role < G::SV;
     // S1V state: this wave walks P rows [a0, a0 + NV) (rows past PH are pad rows that only reach
     // the pad rows of cs); lane = P column c
-    const int a0 = wave * G::RPW;
-    const uint32_t m0_cs = (uint32_t)(a0 * G::CSS * 4);   // cs is the first LDS block
+    const int a0 = (is_s1v ? role : 0) * G::RPW;
+    const uint32_t m0_cs = __builtin_amdgcn_readfirstlane((uint32_t)(a0 * G::CSS * 4));   // cs is the first LDS block
     const int c = lane;
     const int xc = px0 + c;
     const bool col_in = xc >= 0 && xc < W;
@@ -329,11 +349,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // S2V ownership: A column v2j = lane, output rows [8*v2g, 8*v2g + 8) with v2g = wave (one row
     // group per wave: its lanes read one contiguous a/b row span, no bank conflicts at a wrap)
     const bool v2_on = lane < G::AW;
-    const int v2g = wave, v2j = v2_on ? lane : 0;
+    const int v2g = ROLES ? (is_s1v ? 0 : role - G::SV) : wave, v2j = v2_on ? lane : 0;
     const float2* v2col[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        uint32_t off = (uint32_t)(((8 * v2g + k) * G::ABS + v2j) * 8);
+        uint32_t off = (uint32_t)(((G::RPS * v2g + k) * G::ABS + v2j) * 8);
         asm volatile("" : "+v"(off));
         v2col[k] = reinterpret_cast<const float2*>(reinterpret_cast<const uint8_t*>(abp) + off);
     }
@@ -347,7 +367,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // S2H's mm row segment (plane A) as an LDS byte address; plane B is MM_PLANE bytes further
     const uint32_t h2off = (uint32_t)(G::CS_BYTES + (h2r * G::MSA + h2s * G::SW2) * 4);
     // S2V's first mm row of this wave (plane A), for the add-TID stores
-    const uint32_t m0_mm = (uint32_t)(G::CS_BYTES + 8 * wave * G::MSA * 4);
+    const uint32_t m0_mm = __builtin_amdgcn_readfirstlane((uint32_t)(G::CS_BYTES + G::RPS * v2g * G::MSA * 4));
     const int oy = y0 + h2r;
 
     // per-A-pixel constants (filled by the stats pass) and per-output WTA state.
@@ -498,28 +518,42 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         // one ds_read_b64 per row (2 LDS cycles) instead of a merged ds_read2_b64 (8 cycles for the
         // same two rows, MI355X_MICROARCH.md LDS table): rows k and k + 5 share a base whose value the
         // compiler cannot relate to the others, and 5 rows (2160 B) exceed ds_read2's offset range
-        float2 v[8 + 2 * R];   // loaded before the mm stores, as in S1H
+        // RPS output rows in groups of 8: the rows a group adds are loaded at its start (the first group
+        // also loads the 2R warm-up rows), before its mm stores, as in S1H; a row's registers are
+        // free once no later group reads it.  Each group restarts its running sums from its own 2R
+        // warm-up rows, as an 8-row strip does without the roles: the float sums, and so the maps, are
+        // the same bit for bit in every configuration (the right-view kernel runs without the roles,
+        // and the LR check pairs its left map with the left-only kernel's)
+        constexpr int NRW = G::RPS + 2 * R;
+        float2 v[NRW];
 #pragma unroll
         for (int k = 0; k < 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
-        float sa = 0.f, sb = 0.f;
-#pragma unroll
-        for (int k = 0; k < 2 * R; ++k) {
-            sa += v[k].x;
-            sb += v[k].y;
-        }
         // M0 = this wave's first mm row (plane A), set once per call as in S1V
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(m0_mm) : "m0");
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            sa += v[r + 2 * R].x;
-            sb += v[r + 2 * R].y;
-            // mmA / mmB [(8 v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32
-            asm volatile("ds_write_addtid_b32 %0 offset:%2\n\tds_write_addtid_b32 %1 offset:%3"
-                         :
-                         : "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
-                         : "memory");
-            sa -= v[r].x;
-            sb -= v[r].y;
+        for (int g = 0; g < G::RPS / 8; ++g) {
+            if (g > 0) {
+#pragma unroll
+                for (int k = 8 * g + 2 * R; k < 8 * g + 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
+            }
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int k = 8 * g; k < 8 * g + 2 * R; ++k) {
+                sa += v[k].x;
+                sb += v[k].y;
+            }
+#pragma unroll
+            for (int r = 8 * g; r < 8 * g + 8; ++r) {
+                sa += v[r + 2 * R].x;
+                sb += v[r + 2 * R].y;
+                // mmA / mmB [(RPS v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32
+                asm volatile("ds_write_addtid_b32 %0 offset:%2\n\tds_write_addtid_b32 %1 offset:%3"
+                             :
+                             : "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
+                             : "memory");
+                sa -= v[r].x;
+                sb -= v[r].y;
+            }
         }
     };
     // ================= S2H + WTA =================
@@ -574,7 +608,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
     };
-    s1v(0, std::true_type{}, std::false_type{});
+    if (is_s1v) s1v(0, std::true_type{}, std::false_type{});
     const bool s1_nomask = px0 >= D - 1 && px0 >= 0 && px0 + 63 < W;
     const bool s2_lim = valid_mode != 1 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
     lds_barrier();
@@ -584,11 +618,11 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
     // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
     for (int d = d_lo; d <= D; ++d) {
-        if (d < D) {
+        if (is_s1v && d < D) {
             if (s1_nomask) s1v(d, std::false_type{}, std::true_type{});
             else s1v(d, std::false_type{}, std::false_type{});
         }
-        if (d > d_lo) s2v();
+        if ((!ROLES || !is_s1v) && d > d_lo) s2v();
         lds_barrier();
         if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
         if (d < D) s1h();
@@ -681,19 +715,21 @@ template <int R>
 hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch,
                      int d_lo, int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride,
                      int* gpart, uint8_t* right, int rpitch, int64_t rstride, int* keys, hipStream_t s) {
-    using G = GeoF<R>;
+    using G = GeoF<R, false>;   // tile geometry (TW, TH, SW2) is the same with or without the roles
     const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    // the left-only kernel may run the phase-1 wave roles: its LDS plan is GeoF<R, kGuidedRoles>'s
+    constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS, lds_right = (size_t)GeoF<R, false>::LDS;
     if (!gpart) {
-        hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L,
+        hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), lds_left, s, L,
                            Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
                            tiles_x * tiles_y, nullptr, 0, keys);
         return hipGetLastError();
     }
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
-    hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), (size_t)G::LDS, s, L, Rimg,
+    hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), lds_right, s, L, Rimg,
                        W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
                        K, nullptr);
     hipError_t e = hipGetLastError();
@@ -706,7 +742,7 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
 
 template <int R>
 size_t partial_bytes(int W, int H, int D, int batch) {
-    using G = GeoF<R>;
+    using G = GeoF<R, false>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }

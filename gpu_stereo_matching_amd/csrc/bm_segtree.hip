@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kFT) void st_filter_kernel(FilterJobs jobs, int P) 
 // global operands (cost / metadata) are loaded kStPre tasks ahead into a register ring, so the loads of
 // later levels are in flight while a level's LDS chain runs.
 #ifndef SM_ST_PRE
-#define SM_ST_PRE 4
+#define SM_ST_PRE 16
 #endif
 constexpr int kStPre = SM_ST_PRE;
 
