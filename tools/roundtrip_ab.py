@@ -1,5 +1,5 @@
-"""Drop-in host round trip (sm_block_match_u8, 1080p D=128 r=5) on sm_host_alloc frames and map, with and
-without the zero-copy map (SM_ZERO_COPY=0 keeps the download).  Each setting runs in its own process,
+"""Drop-in host round trip (sm_block_match_u8, 1080p D=128 r=5) on sm_host_alloc frames and map: DMA upload +
+download (SM_ZERO_COPY=0) against DMA upload + zero-copy map (the default).  Each setting runs in its own process,
 alternated 3 times; prints the median wall ms per call of each run and the last call's stage split."""
 import os, subprocess, sys, statistics
 if len(sys.argv) > 1 and sys.argv[1] == "child":
@@ -22,17 +22,18 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
             ts.append(time.perf_counter() - t0)
         print("RESULT", statistics.median(ts) * 1e3, *m.stage_ms())
     sys.exit(0)
-res = {"1": [], "0": []}
+SETTINGS = {"dma": {"SM_ZERO_COPY": "0"}, "zc": {"SM_ZERO_COPY": "1"}}
+res = {k: [] for k in SETTINGS}
 for _ in range(3):
-    for zc in ("1", "0"):
-        out = subprocess.run([sys.executable, __file__, "child"], env=dict(os.environ, SM_ZERO_COPY=zc),
+    for zc, env in SETTINGS.items():
+        out = subprocess.run([sys.executable, __file__, "child"], env=dict(os.environ, **env),
                              capture_output=True, text=True, timeout=200)
         line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
         if not line:
             print(out.stdout, out.stderr)
             sys.exit(1)
         res[zc].append([float(v) for v in line[0].split()[1:]])
-for zc, name in (("0", "download (SM_ZERO_COPY=0)"), ("1", "zero-copy map")):
+for zc, name in (("dma", "DMA up + download"), ("zc", "DMA up + zero-copy map")):
     walls = [v[0] for v in res[zc]]
     print(f"{name:28s} wall ms/call median {statistics.median(walls):.4f} all {[round(w, 4) for w in walls]} "
           f"last stages upload/match/download {[round(x, 4) for x in res[zc][-1][1:]]}")

@@ -20,6 +20,12 @@ JOBS = (
 )
 
 
+# issue / wait breakdown of the guided kernels: wave cycles spent waiting at
+# s_waitcnt / barriers (SQ_WAIT_ANY), stalled on issue (SQ_WAIT_INST_ANY; SQ_WAIT_INST_LDS its LDS part)
+# and issuing (SQ_ACTIVE_INST_ANY), which add up to SQ_WAVE_CYCLES
+WAIT_CTRS = "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES"
+
+
 def main():
     env = dict(os.environ, TMPDIR="/tmp")
     tag = os.environ.get("SM_TAG", "")
@@ -38,7 +44,24 @@ def main():
             for row in csv.DictReader(open(f)):
                 if kname in row["Kernel_Name"]:
                     vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        if "guided" in name:
+            d2 = d + "_wait"
+            cmd2 = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc"] + WAIT_CTRS.split() + [
+                "-d", d2, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
+                os.path.join(ROOT, "tools", "kernel_driver.py"), "--iters", "3"] + args
+            if os.environ.get("SM_LIB"):
+                cmd2 += ["--lib", os.environ["SM_LIB"]]
+            subprocess.run(cmd2, check=True, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            for f in glob.glob(os.path.join(d2, "**", "*counter_collection.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    if kname in row["Kernel_Name"]:
+                        vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
         med = {k: statistics.median(v) for k, v in vals.items()}
+        if "SQ_WAVE_CYCLES" in med and med["SQ_WAVE_CYCLES"] > 0:
+            wc = med["SQ_WAVE_CYCLES"]
+            med["share_wait_any"] = med.get("SQ_WAIT_ANY", 0) / wc
+            med["share_wait_inst_any"] = med.get("SQ_WAIT_INST_ANY", 0) / wc
+            med["share_active_inst_any"] = med.get("SQ_ACTIVE_INST_ANY", 0) / wc
         res["kernels"][name] = {"kernel": kname, "workload": wl, "per_launch": med}
         print(name, json.dumps(med), flush=True)
     out = os.path.join(ROOT, "gpurun_out", "valu_counts%s.json" % tag)
