@@ -262,8 +262,13 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 
 // r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere; with the fused right
 // view r = 3 (7 outputs per S2H thread) spills at 168 and also runs at 2
+// SM_G_ROLES_RIGHT (A/B only): the wave roles in the right-view kernel too, at 2 waves/SIMD (its
+// registers do not fit 3 with them)
+#ifndef SM_G_ROLES_RIGHT
+#define SM_G_ROLES_RIGHT 0
+#endif
 template <int R, bool RIGHT>
-constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && R == 3)) ? 2 : 3;
+constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT))) ? 2 : 3;
 
 // right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
 constexpr float kRightScale = 16384.0f;
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
     // wave roles without the fused right view only: its key chain leaves no registers for the taller
     // strips (168-VGPR budget, spills measured in the ISA)
-    constexpr bool ROLES = kGuidedRoles && !RIGHT;
+    constexpr bool ROLES = kGuidedRoles && (!RIGHT || SM_G_ROLES_RIGHT);
     using G = GeoF<R, ROLES>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
@@ -720,7 +725,8 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // the left-only kernel may run the phase-1 wave roles: its LDS plan is GeoF<R, kGuidedRoles>'s
-    constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS, lds_right = (size_t)GeoF<R, false>::LDS;
+    constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS;
+    constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && SM_G_ROLES_RIGHT>::LDS;
     if (!gpart) {
         hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), lds_left, s, L,
                            Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
