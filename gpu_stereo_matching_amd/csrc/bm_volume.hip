@@ -133,12 +133,13 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
 #pragma unroll
         for (int q = 0; q < NQ; ++q) o[q] = absdiff_u8x4(l[q], r[q]);
         if (x0 < d + SEG) {   // bytes with x < d are 0 (Device.cu:27-31 + the memset)
+            // dword q drops its low n = clamp(d - x0 - 4q, 0, 4) bytes: one 64-bit shift per dword (a
+            // per-byte compare + select here cost 8 VALU per dword plus hazard nops, in every wave
+            // holding the row's first segment)
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                uint32_t keep = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) keep |= (x0 + 4 * q + b >= d ? 0xFFu : 0u) << (8 * b);
-                o[q] &= keep;
+                const int n = min(max(d - x0 - 4 * q, 0), 4);
+                o[q] &= (uint32_t)(~0ull << (8 * n));
             }
         }
         uint8_t* dst = out + (int64_t)d * P + x0;
