@@ -210,14 +210,22 @@ __global__ __launch_bounds__(kFT) void st_filter_kernel(FilterJobs jobs, int P) 
 // disparity walks the levels with the two live levels in LDS (ping-pong buffers of the widest
 // level), wave-synchronous: no workgroup barrier and no global store -> load round trip per level,
 // which bound st_filter_kernel (~0.7 us per level).  The host cuts every level into tasks of <= 64
-// nodes (one node per lane): x = first node, y = count | (level parity << 8), z = the level's first
-// node, w = the first node of the level the task reads (children up, parents down).  Each lane's
-// global operands (cost / metadata) are loaded kStPre tasks ahead into a register ring, so the loads of
-// later levels are in flight while a level's LDS chain runs.
-#ifndef SM_ST_PRE
-#define SM_ST_PRE 16
-#endif
-constexpr int kStPre = SM_ST_PRE;
+// nodes (one node per lane), each an int4 {x = first node, count - 1, LDS byte offset of the task's
+// first node in its level buffer, LDS byte offset that the node index of a child (up) / parent (down)
+// is added to}.
+//
+// The tasks run in blocks of kStBlk.  While block b runs, the wave's global loads for block b + 1 (its
+// lanes' node operands) and the records of block b + 2 are in flight; they land in LDS at the end of
+// the block (a wait that is long satisfied by then), where block b + 1 reads them.  Staging through LDS
+// keeps every load and its wait in one loop iteration: a register ring carried across the loop's back
+// edge made the compiler drain all loads (vmcnt(0)) once per trip.  Global memory goes through buffer
+// descriptors (32-bit offsets).
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));   // 16 B in memory (a 3-vector is padded)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int kStBlk = 16;                              // tasks per block: the 64 lanes load 16 int4 records
+constexpr int kStNodeOff = 1024;                        // LDS: [0, 1024) the weight table
+constexpr int kStRecOff = kStNodeOff + kStBlk * 64 * (int)sizeof(u32x3);   // [kStBlk][64 lanes] node operands
+constexpr int kStLvlOff = kStRecOff + 2 * kStBlk * 16;  // [2 blocks][kStBlk] records, then the level buffers
 
 struct WaveJob {
     float* C;                  // in: cost, out: leaf-to-root sums (read again by the root-to-leaf pass)
@@ -228,133 +236,149 @@ struct WaveJob {
     const uint32_t* child;
     const int4* task;          // [n_up tasks, leaf to root][n_dn tasks, root to leaf]
     int n_up, n_dn;
-    int maxw;                  // widest level (LDS buffer length)
+    int maxw;                  // widest level (sizes the LDS; the task records carry the offsets)
     const float* table;
 };
 struct WaveJobs {
     WaveJob j[2];
 };
 
-__global__ __launch_bounds__(64) void st_filter_wave_kernel(WaveJobs jobs, int P) {
+using BufRsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ BufRsrc buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+constexpr int kAuxSc1 = 16;   // sc1: the load misses the (non-coherent) L1, as an agent-scope atomic load
+template <int AUX = 0>
+__device__ __forceinline__ uint32_t buf_ld(BufRsrc r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
+}
+// one wave per CU at most (D or 2 D waves on 256 CUs): the compiler may schedule for latency, not occupancy
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void st_filter_wave_kernel(WaveJobs jobs,
+                                                                                                       int P) {
 #pragma clang fp contract(off)
     const WaveJob& jb = jobs.j[blockIdx.y];
-    extern __shared__ float sbuf[];          // [256] table | [maxw] level buffer 0 | [maxw] level buffer 1
-    float* table = sbuf;
-    float* lvl = sbuf + 256;                 // level buffer of parity q at lvl + q * maxw
-    const int lane = threadIdx.x, maxw = jb.maxw;
-    for (int k = lane; k < 256; k += 64) table[k] = jb.table[k];
-    float* __restrict__ U = jb.C + (int64_t)blockIdx.x * P;
-    float* __restrict__ Fd = jb.F + (int64_t)blockIdx.x * P;
-    const int4* task = jb.task;
+    extern __shared__ float sbuf[];          // layout: kSt*Off above
+    const int lane = threadIdx.x;
+    for (int k = lane; k < 256; k += 64) sbuf[k] = jb.table[k];
+    const uint32_t Pb = (uint32_t)P * 4u;
+    const BufRsrc rU = buf_rsrc(jb.C + (int64_t)blockIdx.x * P, Pb);
+    const BufRsrc rF = buf_rsrc(jb.F + (int64_t)blockIdx.x * P, Pb);
+    char* lds = reinterpret_cast<char*>(sbuf);
+    auto lds_f = [&](int off) -> float& { return *reinterpret_cast<float*>(lds + off); };
+    u32x3* node_area = reinterpret_cast<u32x3*>(lds + kStNodeOff);   // [k][lane]
+    i32x4* rec_area = reinterpret_cast<i32x4*>(lds + kStRecOff);     // [block parity][k]
     __syncthreads();
 
-    // Software pipeline over the tasks, kStPre deep: at task t the wave consumes the node operands
-    // loaded kStPre tasks earlier, issues those of task t + kStPre (its record arrived kStPre tasks
-    // ago) and the record of task t + 2 kStPre.  Every load is unconditional (indices clamped to a
-    // valid task / node), so the compiler's vmcnt waits count exactly the loads still needed.
-    // Records are vector loads of one uniform address; their fields stay in VGPRs.
-    // Records are loaded one dword per lane (lane & 3), so the compiler cannot take them for uniform
-    // values and move them into SGPRs as soon as they are loaded (which waits for the load); the fields
-    // are read out with v_readlane when the record is used, kStPre tasks after its load.
+    // node_load(record) -> u32x3 of this lane's node; body(record, node operands)
     auto pass = [&](const int4* tk0, int nt, auto node_load, auto body) {
         if (nt <= 0) return;
-        const int* tw = reinterpret_cast<const int*>(tk0) + (lane & 3);
-        auto rec_load = [&](int t) { return tw[4 * min(t, nt - 1)]; };
-        auto fields = [&](int v) {
-            return make_int4(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 1),
-                             __builtin_amdgcn_readlane(v, 2), __builtin_amdgcn_readlane(v, 3));
+        const BufRsrc rT = buf_rsrc(tk0, (uint32_t)nt * 16u);
+        // lane l loads dword l & 3 of record (block start + l / 4), clamped to the last task
+        auto rec_block = [&](int blk) {
+            const int t = min(blk * kStBlk + (lane >> 2), nt - 1);
+            return (int)buf_ld(rT, (uint32_t)t * 16u + (uint32_t)(lane & 3) * 4u);
         };
-        using NodeT = decltype(node_load(int4{}));
-        int rec[kStPre], nrec[kStPre];
-        NodeT nd[kStPre];
+        auto rec_put = [&](int parity, int v) { reinterpret_cast<int*>(rec_area + parity * kStBlk)[lane] = v; };
+        const int nb = (nt + kStBlk - 1) / kStBlk;
+        // prologue: records of blocks 0 and 1, node operands of block 0
+        rec_put(0, rec_block(0));
+        const int r1 = rec_block(1);
+        {
+            u32x3 g[kStBlk];
 #pragma unroll
-        for (int k = 0; k < kStPre; ++k) {
-            rec[k] = rec_load(k);
-            nd[k] = node_load(fields(rec[k]));
-            nrec[k] = rec_load(k + kStPre);
+            for (int k = 0; k < kStBlk; ++k) g[k] = node_load(rec_area[k]);
+#pragma unroll
+            for (int k = 0; k < kStBlk; ++k) node_area[k * 64 + lane] = g[k];
         }
-        for (int t0 = 0; t0 < nt; t0 += kStPre) {
+        rec_put(1, r1);
+        for (int b = 0; b < nb; ++b) {
+            const int cur = b & 1;
+            // loads for later blocks: the records of block b + 2, the node operands of block b + 1
+            const int rn = rec_block(b + 2);
+            u32x3 g[kStBlk];
 #pragma unroll
-            for (int k = 0; k < kStPre; ++k) {
-                const int t = t0 + k;
-                if (t < nt) body(fields(rec[k]), nd[k]);
-                __builtin_amdgcn_wave_barrier();
-                rec[k] = nrec[k];
-                nd[k] = node_load(fields(rec[k]));
-                nrec[k] = rec_load(t + 2 * kStPre);
+            for (int k = 0; k < kStBlk; ++k) g[k] = node_load(rec_area[(cur ^ 1) * kStBlk + k]);
+            // block b: its records and node operands all read before the first level write
+            i32x4 rc[kStBlk];
+            u32x3 nd[kStBlk];
+#pragma unroll
+            for (int k = 0; k < kStBlk; ++k) {
+                rc[k] = rec_area[cur * kStBlk + k];
+                nd[k] = node_area[k * 64 + lane];
             }
+            // no branches: a block past the last task repeats the last task (records clamped), which
+            // rewrites the same values
+#pragma unroll
+            for (int k = 0; k < kStBlk; ++k) body(rc[k], nd[k]);
+            // stage block b + 1's operands and block b + 2's records
+#pragma unroll
+            for (int k = 0; k < kStBlk; ++k) node_area[k * 64 + lane] = g[k];
+            rec_put(cur, rn);
         }
     };
-    auto node_of = [&](const int4& r) { return r.x + min(lane, (r.y & 0xFF) - 1); };
+    // byte offset of this lane's node (lanes past the task's count repeat its last node); the store
+    // offset of those lanes lies past the buffer's end, where the hardware drops the store
+    auto node_off = [&](const i32x4& r) { return (uint32_t)(r.x + min(lane, r.y)) * 4u; };
+    auto store_off = [&](const i32x4& r) { return lane <= r.y ? (uint32_t)(r.x + lane) * 4u : 0x80000000u; };
 
     // ---- leaf to root: u = C[i] + sum_z table[dist_z] * u(child z), children in order ----
-    struct UpNode {
-        float c;
-        uint32_t ch;
-        int f;
-    };
-    const uint32_t* __restrict__ child = jb.child;
-    const int* __restrict__ first = jb.first;
-    pass(task, jb.n_up,
-         [&](const int4& r) {
-             const int i = node_of(r);
-             return UpNode{U[i], child[i], first[i]};
+    const BufRsrc rChild = buf_rsrc(jb.child, Pb), rFirst = buf_rsrc(jb.first, Pb);
+    pass(jb.task, jb.n_up,
+         [&](const i32x4& r) {
+             const uint32_t o = node_off(r);
+             return u32x3{buf_ld(rU, o), buf_ld(rChild, o), buf_ld(rFirst, o)};
          },
-         [&](const int4& r, const UpNode& n0) {
-             const int cnt = r.y & 0xFF, q = (r.y >> 8) & 1;
-             if (lane < cnt) {
-                 const float* nxt = lvl + (q ^ 1) * maxw + (n0.f - r.w);
-                 const int n = (int)(n0.ch & 0xFFu);
-                 float u = n0.c;
+         [&](const i32x4& r, const u32x3& n0) {
+             // every lane computes (those past the count into the level buffer's 64-float pad)
+             {
+                 const uint32_t ch = n0.y;
+                 const int n = (int)(ch & 0xFFu);
+                 const int rd = r.w + (int)n0.z * 4;
+                 float u = __builtin_bit_cast(float, n0.x);
                  // at most 3 children (a grid node has 4 neighbours, one of them its parent; the root is
                  // the corner pixel 0): all six LDS reads issued together, absent children's terms dropped
-                 // (their reads stay inside the level buffers)
+                 // (their reads stay inside the level buffer and its pad; reads past the allocation
+                 // return 0)
                  float cv[3], wv[3];
 #pragma unroll
                  for (int z = 0; z < 3; ++z) {
-                     cv[z] = nxt[z < n ? z : 0];
-                     wv[z] = table[(n0.ch >> (8 * (z + 1))) & 0xFFu];
+                     cv[z] = lds_f(rd + 4 * z);
+                     wv[z] = sbuf[(ch >> (8 * (z + 1))) & 0xFFu];
                  }
 #pragma unroll
                  for (int z = 0; z < 3; ++z) {
                      const float tt = cv[z] * wv[z];
                      u = z < n ? u + tt : u;
                  }
-                 lvl[q * maxw + r.x + lane - r.z] = u;
-                 if (n) U[r.x + lane] = u;
+                 lds_f(r.z + lane * 4) = u;
+                 // a leaf's u is its C: rewritten unchanged
+                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, u), rU, store_off(r), 0, 0);
              }
          });
     __syncthreads();   // the U stores have completed (vmcnt) before the root-to-leaf pass reads them back
 
     // ---- root to leaf: F[i] = w (F[parent] - w U[i]) + U[i] ----
-    const int* __restrict__ parent = jb.parent;
-    const uint8_t* __restrict__ pdist = jb.pdist;
     if (lane == 0) {
-        const float u0 = __hip_atomic_load(&U[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        Fd[0] = u0;
-        lvl[0] = u0;   // level 0 (the root) has parity 0
+        const float u0 = __builtin_bit_cast(float, buf_ld<kAuxSc1>(rU, 0));
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, u0), rF, 0, 0, 0);
+        lds_f(kStLvlOff) = u0;   // level 0 (the root) has parity 0
     }
     __builtin_amdgcn_wave_barrier();
-    struct DnNode {
-        float u;
-        int p;
-        uint32_t dd;
-    };
-    pass(task + jb.n_up, jb.n_dn,
-         [&](const int4& r) {
-             const int i = node_of(r);
-             // written by this wave's leaf-to-root pass: read past the (non-coherent) L1
-             return DnNode{__hip_atomic_load(&U[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), parent[i],
-                           (uint32_t)pdist[i]};
+    const BufRsrc rParent = buf_rsrc(jb.parent, Pb), rDist = buf_rsrc(jb.pdist, (uint32_t)P);
+    pass(jb.task + jb.n_up, jb.n_dn,
+         [&](const i32x4& r) {
+             const uint32_t o = node_off(r);
+             // U was written by this wave's leaf-to-root pass: read past the (non-coherent) L1
+             return u32x3{buf_ld<kAuxSc1>(rU, o), buf_ld(rParent, o),
+                          (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rDist, o >> 2, 0, 0)};
          },
-         [&](const int4& r, const DnNode& n0) {
-             const int cnt = r.y & 0xFF, q = (r.y >> 8) & 1;
-             if (lane < cnt) {
-                 const float w = table[n0.dd], u = n0.u;
+         [&](const i32x4& r, const u32x3& n0) {
+             {
+                 const float w = sbuf[n0.z], u = __builtin_bit_cast(float, n0.x);
                  const float tt = w * u;
-                 const float fv = w * (lvl[(q ^ 1) * maxw + n0.p - r.w] - tt) + u;
-                 lvl[q * maxw + r.x + lane - r.z] = fv;
-                 Fd[r.x + lane] = fv;
+                 const float fv = w * (lds_f(r.w + (int)n0.y * 4) - tt) + u;
+                 lds_f(r.z + lane * 4) = fv;
+                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, fv), rF, store_off(r), 0, 0);
              }
          });
 }
@@ -440,16 +464,25 @@ FilterJob filter_job(float* C, float* F, const DevTree& d) {
     return FilterJob{C, F, d.parent, d.pdist, d.first, d.child, d.lev, d.nlev, d.table};
 }
 
+// a level buffer holds the widest level and 64 floats of pad for the lanes past a task's count
+int wave_level_stride(int maxw) { return maxw + 64; }
+
 // The wave filter's tasks of one tree (st_filter_wave_kernel): every level cut into runs of <= 64 nodes,
-// leaf to root, then root to leaf from level 1.  Returns the widest level.
+// leaf to root, then root to leaf from level 1; each task {first node, count - 1, LDS byte offset of its
+// first node in the level buffer of its level's parity, LDS byte offset that the index of a node of the
+// level it reads (children up, parents down; the other parity's buffer) is added to}.  Returns the
+// widest level, which sizes the buffers.
 int wave_tasks(const HostTree& t, std::vector<int4>& out, int& n_up, int& n_dn) {
     const int nlev = (int)t.lev.size() - 1;
     out.clear();
     int maxw = 1;
+    for (int l = 0; l < nlev; ++l) maxw = std::max(maxw, t.lev[l + 1] - t.lev[l]);
+    const int stride = wave_level_stride(maxw);
     auto cut = [&](int l, int other) {
-        const int lo = t.lev[l], hi = t.lev[l + 1];
-        maxw = std::max(maxw, hi - lo);
-        for (int s0 = lo; s0 < hi; s0 += 64) out.push_back(make_int4(s0, std::min(64, hi - s0) | ((l & 1) << 8), lo, other));
+        const int lo = t.lev[l], hi = t.lev[l + 1], q = l & 1;
+        const int rb = kStLvlOff + ((q ^ 1) * stride - other) * 4;
+        for (int s0 = lo; s0 < hi; s0 += 64)
+            out.push_back(make_int4(s0, std::min(64, hi - s0) - 1, kStLvlOff + (q * stride + s0 - lo) * 4, rb));
     };
     for (int l = nlev - 1; l >= 0; --l) cut(l, l + 1 < nlev ? t.lev[l + 1] : t.lev[l]);
     n_up = (int)out.size();
@@ -458,7 +491,7 @@ int wave_tasks(const HostTree& t, std::vector<int4>& out, int& n_up, int& n_dn) 
     return maxw;
 }
 
-constexpr int kWaveMaxLevel = 7936;   // (256 + 2 * 7936) floats = 64 KB of LDS; wider trees keep st_filter_kernel
+constexpr int kWaveMaxLevel = (65536 - kStLvlOff) / 8 - 64;   // 64 KB of LDS; wider trees keep st_filter_kernel
 
 // Host task list `tv` of tree `d` into task slot k (`per` int4 each) of the workspace, which the caller
 // has grown for all its slots before the first upload; tv must stay alive until the copy has run.
@@ -477,7 +510,7 @@ hipError_t upload_wave_job(StWorkspace& ws, int k, size_t per, const std::vector
 hipError_t launch_filter(const FilterJobs& fj, const WaveJobs& wj, int njobs, int maxw, int D, int P, hipStream_t s) {
     if (maxw <= kWaveMaxLevel) {
         hipLaunchKernelGGL(st_filter_wave_kernel, dim3((unsigned)D, (unsigned)njobs), dim3(64),
-                           (size_t)(256 + 2 * maxw) * sizeof(float), s, wj, P);
+                           (size_t)kStLvlOff + (size_t)(2 * wave_level_stride(maxw)) * sizeof(float), s, wj, P);
     } else {
         hipLaunchKernelGGL(st_filter_kernel, dim3((unsigned)D, (unsigned)njobs), dim3(kFT), 0, s, fj, P);
     }
