@@ -225,7 +225,8 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kStBlk = 16;                              // tasks per block: the 64 lanes load 16 int4 records
 constexpr int kStNodeOff = 1024;                        // LDS: [0, 1024) the weight table
 constexpr int kStRecOff = kStNodeOff + kStBlk * 64 * (int)sizeof(u32x3);   // [kStBlk][64 lanes] node operands
-constexpr int kStLvlOff = kStRecOff + 2 * kStBlk * 16;  // [2 blocks][kStBlk] records, then the level buffers
+constexpr int kStZeroOff = kStRecOff + 2 * kStBlk * 16;  // [2 blocks][kStBlk] records, then a float 0
+constexpr int kStLvlOff = kStZeroOff + 16;               // then the level buffers
 
 struct WaveJob {
     float* C;                  // in: cost, out: leaf-to-root sums (read again by the root-to-leaf pass)
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     extern __shared__ float sbuf[];          // layout: kSt*Off above
     const int lane = threadIdx.x;
     for (int k = lane; k < 256; k += 64) sbuf[k] = jb.table[k];
+    if (lane == 0) sbuf[kStZeroOff / 4] = 0.0f;
     const uint32_t Pb = (uint32_t)P * 4u;
     const BufRsrc rU = buf_rsrc(jb.C + (int64_t)blockIdx.x * P, Pb);
     const BufRsrc rF = buf_rsrc(jb.F + (int64_t)blockIdx.x * P, Pb);
@@ -279,14 +281,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             return (int)buf_ld(rT, (uint32_t)t * 16u + (uint32_t)(lane & 3) * 4u);
         };
         auto rec_put = [&](int parity, int v) { reinterpret_cast<int*>(rec_area + parity * kStBlk)[lane] = v; };
+        // the node loads of a block need each record's first node and count - 1: one LDS dword per lane
+        // (lane l: dword l & 3 of record l / 4) read out with v_readlane, rather than 16 128-bit reads
+        // whose registers the compiler overlaps (and then serialises)
+        auto gather = [&](int parity, u32x3* g) {
+            const int rv = reinterpret_cast<const int*>(rec_area + parity * kStBlk)[lane];
+#pragma unroll
+            for (int k = 0; k < kStBlk; ++k) {
+                i32x4 rr;
+                rr.x = __builtin_amdgcn_readlane(rv, 4 * k);
+                rr.y = __builtin_amdgcn_readlane(rv, 4 * k + 1);
+                rr.z = rr.w = 0;
+                g[k] = node_load(rr);
+            }
+        };
         const int nb = (nt + kStBlk - 1) / kStBlk;
         // prologue: records of blocks 0 and 1, node operands of block 0
         rec_put(0, rec_block(0));
         const int r1 = rec_block(1);
         {
             u32x3 g[kStBlk];
-#pragma unroll
-            for (int k = 0; k < kStBlk; ++k) g[k] = node_load(rec_area[k]);
+            gather(0, g);
 #pragma unroll
             for (int k = 0; k < kStBlk; ++k) node_area[k * 64 + lane] = g[k];
         }
@@ -296,8 +311,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             // loads for later blocks: the records of block b + 2, the node operands of block b + 1
             const int rn = rec_block(b + 2);
             u32x3 g[kStBlk];
-#pragma unroll
-            for (int k = 0; k < kStBlk; ++k) g[k] = node_load(rec_area[(cur ^ 1) * kStBlk + k]);
+            gather(cur ^ 1, g);
             // block b: its records and node operands all read before the first level write
             i32x4 rc[kStBlk];
             u32x3 nd[kStBlk];
@@ -336,19 +350,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                  const int rd = r.w + (int)n0.z * 4;
                  float u = __builtin_bit_cast(float, n0.x);
                  // at most 3 children (a grid node has 4 neighbours, one of them its parent; the root is
-                 // the corner pixel 0): all six LDS reads issued together, absent children's terms dropped
-                 // (their reads stay inside the level buffer and its pad; reads past the allocation
-                 // return 0)
+                 // the corner pixel 0): all six LDS reads issued together.  An absent child reads the
+                 // float 0 (its distance byte is 0, weight 1): its term is +0, and u + 0 = u exactly for the
+                 // non-negative sums here, so the chain after the reads is one multiply and three adds.
                  float cv[3], wv[3];
 #pragma unroll
                  for (int z = 0; z < 3; ++z) {
-                     cv[z] = lds_f(rd + 4 * z);
+                     cv[z] = lds_f(z < n ? rd + 4 * z : kStZeroOff);
                      wv[z] = sbuf[(ch >> (8 * (z + 1))) & 0xFFu];
                  }
 #pragma unroll
                  for (int z = 0; z < 3; ++z) {
                      const float tt = cv[z] * wv[z];
-                     u = z < n ? u + tt : u;
+                     u = u + tt;
                  }
                  lds_f(r.z + lane * 4) = u;
                  // a leaf's u is its C: rewritten unchanged

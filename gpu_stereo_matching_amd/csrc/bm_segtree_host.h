@@ -67,9 +67,13 @@ struct Edge {
 // right edge of b-1 (weight wr[b-1]) and (b+W, b) the upper edge of b+W (weight wu[b+W]).
 template <class F>
 void each_edge(int W, int P, F&& f) {
-    for (int b = 0; b < P; ++b) {
-        if (b % W >= 1) f(b - 1, b, 0);
-        if (b + W < P) f(b + W, b, 1);
+    for (int y0 = 0; y0 < P; y0 += W) {
+        const int ye = std::min(y0 + W, P), up = P - W;   // b + W < P  <=>  b < up
+        if (y0 < up) f(y0 + W, y0, 1);
+        for (int b = y0 + 1; b < ye; ++b) {
+            f(b - 1, b, 0);
+            if (b < up) f(b + W, b, 1);
+        }
     }
 }
 
@@ -161,21 +165,23 @@ SM_ST_NO_CONTRACT
     t.pdist.assign(P, 0);
     t.child.assign(P, 0);
     t.lev.assign(1, 0);
-    std::vector<uint8_t> vis(P, 0);
-    vis[0] = 1;
+    // the marked edges form a forest, so a node's neighbours other than its parent are exactly the ones
+    // BFS has not visited yet (SegmentTree.cpp:116's visited test): compare with the parent's pixel
+    std::vector<int> ppix(P);
+    ppix[0] = -1;
     int end = 1;
     for (int lo = 0, hi = 1; lo < hi; lo = hi, hi = end) {
         t.lev.push_back(hi);
         for (int i = lo; i < hi; ++i) {
-            const int p = t.node[i];
+            const int p = t.node[i], pp = ppix[i];
             t.rank[p] = i;
             t.first[i] = end;
             uint32_t ch = 0, n = 0;
             const Adj& A = adj[p];
             for (int k = 0; k < A.n; ++k) {
                 const int q = A.q[k];
-                if (vis[q]) continue;
-                vis[q] = 1;
+                if (q == pp) continue;
+                ppix[end] = p;
                 const uint8_t dis = A.d[k];
                 ch |= (uint32_t)dis << (8 * (n + 1));
                 ++n;
