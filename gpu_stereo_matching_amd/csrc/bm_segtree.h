@@ -16,7 +16,10 @@ struct StWorkspace {
     uint8_t* tree_b = nullptr; // P per tree: distance to the parent
     float* table = nullptr;    // 256 per tree: exp(-i / (255 sigma))
     int* task = nullptr;       // per tree: the wave filter's level tasks (int4 each), up to 2 * (P + levels)
-    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0;
+    uint32_t* sortbuf = nullptr;   // edge sort: keys and values (2 x 2 nE), digit counts, sorted edges (3 nE)
+    void* h_edges[2] = {nullptr, nullptr};   // page-locked host copies of sorted edges (12 B each), 2 trees
+    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0, sortbuf_n = 0;
+    size_t h_edges_n[2] = {0, 0};
     ~StWorkspace();
     void release();
 };

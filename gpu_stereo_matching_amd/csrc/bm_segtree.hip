@@ -415,6 +415,163 @@ __global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F
     out[p] = (uint8_t)min(m * scale, 255);
 }
 
+// ---- the edge order on the GPU: SegmentTree.cpp:44-69's edges sorted by edge::operator< (weight, then
+// b, then a; SegmentTree.h:103-111) ----
+// Edges are generated in (b, a) order and sorted stably by weight (LSD radix, 8-bit digits: one pass for
+// the integer colour weights, four for the colour + depth floats, whose non-negative values order as
+// their bits), which is that order.  Edge index of pixel b = (y, x): in a row y < H - 1 the edges of b
+// are (b - 1, b) for x >= 1 then (b + W, b), so row y starts at y (2W - 1); the last row has (b - 1, b)
+// only.  Value = 2 b + (edge is (b + W, b)).
+__host__ __device__ inline int64_t st_edge_count(int W, int H) { return (int64_t)(H - 1) * (2 * W - 1) + (W - 1); }
+
+// DEPTH = false: key = colour weight (u8); DEPTH = true: CColorDepthWeight::GetWeight (SegmentTree.cpp:
+// 204-219) from the colour weight, the first left map and its mask, in the reference's float steps
+// (as st_host::depth_weights), key = the float's bits.
+template <bool DEPTH>
+__global__ __launch_bounds__(kST) void st_edge_keys_kernel(const uint8_t* __restrict__ wr, const uint8_t* __restrict__ wu,
+                                                           const uint8_t* __restrict__ disp,
+                                                           const uint8_t* __restrict__ mask, float level, int W, int H,
+                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+#pragma clang fp contract(off)
+    const int x = blockIdx.x * kST + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int b = y * W + x;
+    auto key = [&](int a, int q, uint8_t c) -> uint32_t {
+        if constexpr (DEPTH) {
+            float w;
+            if (mask[a] && mask[q]) {
+                const float dispValue = (float)abs((int)disp[a] - (int)disp[q]) / level;
+                const float colorValue = (float)c / 255.0f;
+                w = 0.5f * dispValue + (1.0f - 0.5f) * colorValue;
+            } else {
+                w = (float)c / 255.0f;
+            }
+            return __builtin_bit_cast(uint32_t, w);
+        } else {
+            return c;
+        }
+    };
+    const int64_t base = (int64_t)y * (2 * W - 1);
+    if (y < H - 1) {
+        if (x >= 1) {
+            keys[base + 2 * x - 1] = key(b - 1, b, wr[b - 1]);   // (b - 1, b): right edge of b - 1
+            vals[base + 2 * x - 1] = 2u * (uint32_t)b;
+        }
+        const int64_t iu = x >= 1 ? base + 2 * x : base;
+        keys[iu] = key(b + W, b, wu[b + W]);                     // (b + W, b): upper edge of b + W
+        vals[iu] = 2u * (uint32_t)b + 1u;
+    } else if (x >= 1) {
+        keys[base + x - 1] = key(b - 1, b, wr[b - 1]);
+        vals[base + x - 1] = 2u * (uint32_t)b;
+    }
+}
+
+// one radix pass: single-wave blocks of kRxIPB consecutive items, 64 per round
+constexpr int kRxRounds = 32;
+constexpr int kRxIPB = 64 * kRxRounds;
+
+__global__ __launch_bounds__(64) void st_rx_hist_kernel(const uint32_t* __restrict__ keys, int n, int shift,
+                                                        uint32_t* __restrict__ hist, int nb) {
+    __shared__ uint32_t h[256];
+    const int lane = threadIdx.x, blk = blockIdx.x;
+    for (int k = lane; k < 256; k += 64) h[k] = 0;
+    __syncthreads();
+    for (int r = 0; r < kRxRounds; ++r) {
+        const int i = blk * kRxIPB + r * 64 + lane;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    for (int k = lane; k < 256; k += 64) hist[(size_t)k * nb + blk] = h[k];
+}
+
+// exclusive scan of the digit-major counts [256][nb]: each digit's row scanned over the blocks by one
+// wave (st_rx_scan_rows_kernel, also writing the row total), then the 256 totals by one wave into the
+// digits' bases (st_rx_scan_bases_kernel), which the scatter adds
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(v, off, 64);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+__global__ __launch_bounds__(64) void st_rx_scan_rows_kernel(uint32_t* __restrict__ hist, int nb,
+                                                             uint32_t* __restrict__ total) {
+    const int lane = threadIdx.x, dg = blockIdx.x;
+    uint32_t* row = hist + (size_t)dg * nb;
+    uint32_t run = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        const uint32_t c = b < nb ? row[b] : 0u;
+        const uint32_t inc = wave_incl_scan(c, lane);
+        if (b < nb) row[b] = run + inc - c;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) total[dg] = run;
+}
+__global__ __launch_bounds__(64) void st_rx_scan_bases_kernel(uint32_t* __restrict__ total) {
+    const int lane = threadIdx.x;
+    uint32_t run = 0;
+    for (int d0 = 0; d0 < 256; d0 += 64) {
+        const uint32_t c = total[d0 + lane];
+        const uint32_t inc = wave_incl_scan(c, lane);
+        total[d0 + lane] = run + inc - c;
+        run += __shfl(inc, 63, 64);
+    }
+}
+
+// stable scatter of one pass: an item's position = its digit's offset for the block + the items of the
+// same digit before it in the block (earlier rounds: the running counts cnt; this round: the lanes below
+// it whose 8 digit bits all agree, from 8 ballots).  FINAL: write the edge records {a, b, w} instead of
+// keys and values.
+template <bool FINAL, bool DEPTH>
+__global__ __launch_bounds__(64) void st_rx_scatter_kernel(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                           int n, int shift, const uint32_t* __restrict__ hist,
+                                                           const uint32_t* __restrict__ bases, int nb,
+                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                           st_host::Edge* __restrict__ eout, int W) {
+    __shared__ uint32_t cnt[256];
+    const int lane = threadIdx.x, blk = blockIdx.x;
+    for (int k = lane; k < 256; k += 64) cnt[k] = bases[k] + hist[(size_t)k * nb + blk];
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int r = 0; r < kRxRounds; ++r) {
+        const int i = blk * kRxIPB + r * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
+        const uint32_t dg = (k >> shift) & 0xFFu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool on = (dg >> bit) & 1u;
+            const uint64_t bb = __ballot(on);
+            peers &= on ? bb : ~bb;
+        }
+        const uint32_t base = cnt[dg];
+        __builtin_amdgcn_wave_barrier();
+        // the lowest lane of each digit group advances the digit's count (after every lane has read it)
+        if (valid && (peers & lt) == 0) cnt[dg] = base + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        if (valid) {
+            const uint32_t pos = base + (uint32_t)__popcll(peers & lt);
+            if constexpr (FINAL) {
+                const int b = (int)(v >> 1);
+                eout[pos] = st_host::Edge{(v & 1u) ? b + W : b - 1, b,
+                                          DEPTH ? __builtin_bit_cast(float, k) : (float)k};
+            } else {
+                kout[pos] = k;
+                vout[pos] = v;
+            }
+        }
+    }
+}
+
+// The sorted edges of one tree into page-locked host slot `slot` of the workspace (asynchronous on s).
+// DEPTH: colour + depth weights from the left map `disp` and its mask.
+hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* wu, const uint8_t* disp,
+                            const uint8_t* mask, float level, int W, int H, bool depth, int slot, hipStream_t s,
+                            int& nE);
+
 // ---- host: the tree, sequential as the reference's (bm_segtree_host.h) ----
 using namespace st_host;
 
@@ -427,6 +584,60 @@ hipError_t grow(T*& p, size_t& have, size_t n) {
     hipError_t e = hipMalloc(&p, n * sizeof(T));
     if (e == hipSuccess) have = n;
     return e;
+}
+
+hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* wu, const uint8_t* disp,
+                            const uint8_t* mask, float level, int W, int H, bool depth, int slot, hipStream_t s,
+                            int& nE) {
+    const int64_t n64 = st_edge_count(W, H);
+    if (n64 <= 0 || n64 > (1 << 30)) return hipErrorInvalidValue;
+    const int n = (int)n64, nb = (n + kRxIPB - 1) / kRxIPB;
+    // keys / values x 2, digit counts, edge records (3 dwords each)
+    const size_t need = (size_t)4 * n + (size_t)256 * (nb + 1) + (size_t)3 * n;
+    hipError_t e;
+    if ((e = grow(ws.sortbuf, ws.sortbuf_n, need)) != hipSuccess) return e;
+    const size_t hbytes = (size_t)n * sizeof(st_host::Edge);
+    if (ws.h_edges_n[slot] < hbytes) {
+        if (ws.h_edges[slot]) (void)hipHostFree(ws.h_edges[slot]);
+        ws.h_edges[slot] = nullptr;
+        ws.h_edges_n[slot] = 0;
+        if ((e = hipHostMalloc(&ws.h_edges[slot], hbytes, hipHostMallocDefault)) != hipSuccess) return e;
+        ws.h_edges_n[slot] = hbytes;
+    }
+    uint32_t* k0 = ws.sortbuf;
+    uint32_t* v0 = k0 + n;
+    uint32_t* k1 = v0 + n;
+    uint32_t* v1 = k1 + n;
+    uint32_t* hist = v1 + n;
+    uint32_t* bases = hist + (size_t)256 * nb;
+    auto* edges = reinterpret_cast<st_host::Edge*>(bases + 256);
+    const dim3 rows((unsigned)((W + kST - 1) / kST), (unsigned)H);
+    if (depth)
+        hipLaunchKernelGGL(st_edge_keys_kernel<true>, rows, dim3(kST), 0, s, wr, wu, disp, mask, level, W, H, k0, v0);
+    else
+        hipLaunchKernelGGL(st_edge_keys_kernel<false>, rows, dim3(kST), 0, s, wr, wu, disp, mask, level, W, H, k0, v0);
+    const int passes = depth ? 4 : 1;
+    for (int ps = 0; ps < passes; ++ps) {
+        const int shift = 8 * ps;
+        hipLaunchKernelGGL(st_rx_hist_kernel, dim3((unsigned)nb), dim3(64), 0, s, k0, n, shift, hist, nb);
+        hipLaunchKernelGGL(st_rx_scan_rows_kernel, dim3(256), dim3(64), 0, s, hist, nb, bases);
+        hipLaunchKernelGGL(st_rx_scan_bases_kernel, dim3(1), dim3(64), 0, s, bases);
+        if (ps + 1 < passes) {
+            hipLaunchKernelGGL((st_rx_scatter_kernel<false, false>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
+                               hist, bases, nb, k1, v1, edges, W);
+            std::swap(k0, k1);
+            std::swap(v0, v1);
+        } else if (depth) {
+            hipLaunchKernelGGL((st_rx_scatter_kernel<true, true>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
+                               hist, bases, nb, k1, v1, edges, W);
+        } else {
+            hipLaunchKernelGGL((st_rx_scatter_kernel<true, false>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
+                               hist, bases, nb, k1, v1, edges, W);
+        }
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    nE = n;
+    return hipMemcpyAsync(ws.h_edges[slot], edges, hbytes, hipMemcpyDeviceToHost, s);
 }
 
 // One tree on the device: workspace slot k holds int [rank | parent | first | child | lev] (5P + 2),
@@ -548,6 +759,14 @@ void StWorkspace::release() {
     (void)hipFree(table);
     (void)hipFree(task);
     task = nullptr;
+    (void)hipFree(sortbuf);
+    sortbuf = nullptr;
+    sortbuf_n = 0;
+    for (int k = 0; k < 2; ++k) {
+        if (h_edges[k]) (void)hipHostFree(h_edges[k]);
+        h_edges[k] = nullptr;
+        h_edges_n[k] = 0;
+    }
     w8 = nullptr;
     grad = nullptr;
     vol = nullptr;
@@ -580,8 +799,9 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     uint8_t* wu = ws.w8 + P;
     hipLaunchKernelGGL(st_weights_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, wr, wu);
     ST_CHK(hipGetLastError());
-    std::vector<uint8_t> hw((size_t)P * 2);
-    ST_CHK(hipMemcpyAsync(hw.data(), ws.w8, (size_t)P * 2, hipMemcpyDeviceToHost, s));
+    // the edges in the reference's order, sorted on the GPU, -> host
+    int nE = 0;
+    ST_CHK(gpu_sorted_edges(ws, wr, wu, nullptr, nullptr, 0.f, W, H, false, 0, s, nE));
     // gradients of both views meanwhile (same stream, after the download in order)
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
@@ -590,7 +810,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     // tree on the host
     const auto t0 = std::chrono::steady_clock::now();
     HostTree t;
-    if (!build_tree(hw.data(), hw.data() + P, W, H, tau, t)) return hipErrorInvalidValue;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 1.0f, t)) return hipErrorInvalidValue;
     float table[256];
     weight_table(sigma, table);
     const float tree_ms = ms_since(t0);
@@ -650,8 +870,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     hipLaunchKernelGGL(st_weights_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, wrL, wrL + P);
     hipLaunchKernelGGL(st_weights_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, wrR, wrR + P);
     ST_CHK(hipGetLastError());
-    std::vector<uint8_t> hw((size_t)P * 4);
-    ST_CHK(hipMemcpyAsync(hw.data(), ws.w8, (size_t)P * 4, hipMemcpyDeviceToHost, s));
+    // both views' edges in the reference's order, sorted on the GPU, -> host
+    int nE = 0;
+    ST_CHK(gpu_sorted_edges(ws, wrL, wrL + P, nullptr, nullptr, 0.f, W, H, false, 0, s, nE));
+    ST_CHK(gpu_sorted_edges(ws, wrR, wrR + P, nullptr, nullptr, 0.f, W, H, false, 1, s, nE));
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
     ST_CHK(hipGetLastError());
@@ -664,14 +886,14 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // be destroyed): a failed build reports false
     std::thread th([&] {
         try {
-            okR = build_tree(hw.data() + 2 * P, hw.data() + 3 * P, W, H, tau, tr);
+            okR = tree_from_edges(static_cast<Edge*>(ws.h_edges[1]), nE, (int)P, tau, 1.0f, tr);
         } catch (...) {
             okR = false;
         }
     });
     bool okL = false;
     try {
-        okL = build_tree(hw.data(), hw.data() + P, W, H, tau, tl);
+        okL = tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 1.0f, tl);
     } catch (...) {
         okL = false;
     }
@@ -711,17 +933,13 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(launch_median(raw1, W, H, W, P, 1, 3, mapR, W, P, s));
     // left-right check (StereoDisparity.cpp:129-147): mask = !occluded
     ST_CHK(launch_lr_check(mapL, W, P, mapR, W, P, 0, W, H, 1, chk, W, P, nullptr, mask, W, P, s));
-    std::vector<uint8_t> hmap((size_t)P), hmask((size_t)P);
-    ST_CHK(hipMemcpyAsync(hmap.data(), mapL, (size_t)P, hipMemcpyDeviceToHost, s));
-    ST_CHK(hipMemcpyAsync(hmask.data(), mask, (size_t)P, hipMemcpyDeviceToHost, s));
+    // re-segmentation: colour + depth tree on the left view (StereoDisparity.cpp:150-152), its weights
+    // from the first left map and mask, sorted on the GPU
+    ST_CHK(gpu_sorted_edges(ws, wrL, wrL + P, mapL, mask, (float)D, W, H, true, 0, s, nE));
     ST_CHK(hipStreamSynchronize(s));
-    // re-segmentation: colour + depth tree on the left view (StereoDisparity.cpp:150-152)
     t0 = std::chrono::steady_clock::now();
-    std::vector<float> fw((size_t)P * 2);
-    depth_weights(hw.data(), hw.data() + P, hmap.data(), hmask.data(), W, H, (float)D, fw.data(), fw.data() + P);
-    std::vector<Edge> e = sorted_edges_f(fw.data(), fw.data() + P, W, (int)P);
     HostTree td;
-    if (!tree_from_edges(e, (int)P, tau, 255.0f, td)) return hipErrorInvalidValue;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 255.0f, td)) return hipErrorInvalidValue;
     float tab2[256];
     weight_table(sigma, tab2);
     tree_ms += ms_since(t0);

@@ -109,12 +109,12 @@ std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P)
     return e;
 }
 
-// BuildSegmentTree (SegmentTree.cpp:38-139) from sorted edges (consumed): segment_graph, the neighbour
+// BuildSegmentTree (SegmentTree.cpp:38-139) from the nE sorted edges e (consumed: the cross-segment
+// penalty is added in place): segment_graph, the neighbour
 // lists with dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255 colour + depth),
 // BFS from pixel 0, level by level.
-bool tree_from_edges(std::vector<Edge>& e, int P, float tau, float wscale, HostTree& t) {
+bool tree_from_edges(Edge* e, int nE, int P, float tau, float wscale, HostTree& t) {
 SM_ST_NO_CONTRACT
-    const int nE = (int)e.size();
     // segment_graph (segment-graph.h:48-101)
     Dsu u(P);
     std::vector<float> thr(P, tau / 1);
@@ -198,7 +198,7 @@ SM_ST_NO_CONTRACT
 
 bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
     std::vector<Edge> e = sorted_edges_u8(wr, wu, W, W * H);
-    return tree_from_edges(e, W * H, tau, 1.0f, t);
+    return tree_from_edges(e.data(), (int)e.size(), W * H, tau, 1.0f, t);
 }
 
 // CColorDepthWeight::GetWeight (SegmentTree.cpp:204-219) from the colour weights (max channel |diff| on
