@@ -37,6 +37,10 @@ template <bool RIGHT, int R>
 constexpr bool kWideRight = RIGHT && R >= 1 && R <= 6;
 template <bool RIGHT, int R>
 constexpr int kWaves = kWideRight<RIGHT, R> ? 8 : 4;
+// d_max 192 with the right view: 8 waves need 90 KB of LDS (one workgroup per CU, 8 waves); 6 waves
+// need 81.6 KB, so two workgroups fit the 160 KB (12 waves per CU, 3 per SIMD: 168 VGPRs)
+template <bool RIGHT, int R, int DMAX>
+constexpr int kWavesD = (kWideRight<RIGHT, R> && DMAX == 192) ? 6 : kWaves<RIGHT, R>;
 // right-view scatter: pair the two candidates of one u in registers (one ds_min per u) except where
 // the extra live values push the fused loop past 128 VGPRs (r = 3: NQ = 16)
 template <int R>
@@ -124,8 +128,8 @@ constexpr uint32_t kSelW = 0x0C0C0504u;
 // NW = kWideTile (16 waves, one workgroup per CU) for launches of few tiles: the d range of a tile is
 // split over 4x the waves, so a launch of ~1 round of workgroups runs in ~4 short rounds instead.
 constexpr int kWideTile = 16;
-template <int R, int DMAX, bool RIGHT, int NW = kWaves<RIGHT, R>>
-__global__ __launch_bounds__((64 * NW), (NW == kWideTile ? 4 : kMinWavesPerEU<RIGHT, R>))
+template <int R, int DMAX, bool RIGHT, int NW = kWavesD<RIGHT, R, DMAX>>
+__global__ __launch_bounds__((64 * NW), (NW == kWideTile ? 4 : NW == 6 ? 3 : kMinWavesPerEU<RIGHT, R>))
 void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     constexpr int kThreads = 64 * NW;
     using G = Geo<R, DMAX, NW>;
@@ -503,13 +507,13 @@ bool wide_tiles_enabled() {
 
 template <int R, int DMAX, bool RIGHT>
 hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStream_t s) {
-    using G = Geo<R, DMAX, kWaves<RIGHT, R>>;
+    using G = Geo<R, DMAX, kWavesD<RIGHT, R, DMAX>>;
     const int tiles_x = (a.W + G::TW - 1) / G::TW;
     const int tiles_y = (a.H + kTileH - 1) / kTileH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     if constexpr (RIGHT) {
-        hipLaunchKernelGGL((box_match_kernel<R, DMAX, true>), dim3((unsigned)blocks), dim3(64 * kWaves<true, R>),
+        hipLaunchKernelGGL((box_match_kernel<R, DMAX, true>), dim3((unsigned)blocks), dim3(64 * kWavesD<true, R, DMAX>),
                            (size_t)G::LDS_BYTES_R, s, a, tiles_x, tiles_y);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -1,14 +1,15 @@
 """Time one libsm_hip.so build (path as argv[1]) on the 1080p D=128 workload; env SM_AB_R / SM_AB_D /
-SM_AB_B / SM_AB_LR / SM_AB_AGG select radius, disparities, frames per call, LR and aggregation."""
+SM_AB_B / SM_AB_LR / SM_AB_AGG / SM_AB_W / SM_AB_H select radius, disparities, frames per call, LR and aggregation."""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import gpu_stereo_matching_amd._capi as C
 C.load(sys.argv[1])
 import gpu_stereo_matching_amd as sm
-m = sm.BlockMatcher(0, 1920, 1080, 256)
+AW, AH = int(os.environ.get('SM_AB_W', '1920')), int(os.environ.get('SM_AB_H', '1080'))
+m = sm.BlockMatcher(0, AW, AH, 256)
 NB = int(os.environ.get('SM_AB_B', '4'))
-pairs = [sm.synth_pair(1234 + i, 1920, 1080, 128) for i in range(NB)]
+pairs = [sm.synth_pair(1234 + i, AW, AH, 128) for i in range(NB)]
 Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda(); Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
 out = torch.empty_like(Lt)
 LR = bool(int(os.environ.get('SM_AB_LR', '0')))
