@@ -64,6 +64,7 @@ hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride
 hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int64_t fstride, int batch,
                             int D, uint8_t* dif, int64_t dstride, hipStream_t s);
 // staged box path (bm_staged.hip): u16 SAD volume from the AD volume, and WTA over the SAD volume
+// `ad` must have 8 readable bytes past its last plane (ensure_vol pads the handle's volume)
 hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, int D, uint16_t* sad, hipStream_t s);
 // (`frames` consecutive frames of D planes each; frame f's map at disp + f * out_stride)
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,

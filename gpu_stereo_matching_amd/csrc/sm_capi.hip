@@ -175,7 +175,8 @@ int ensure_vol(sm_handle* h, size_t bytes) {
     if (h->d_vol) (void)hipFree(h->d_vol);
     h->d_vol = nullptr;
     h->vol_bytes = 0;
-    SM_HIP(hipMalloc(&h->d_vol, bytes));
+    // 64 readable bytes past the end: box_sad_kernel reads whole 8-byte words at the planes' last bytes
+    SM_HIP(hipMalloc(&h->d_vol, bytes + 64));
     h->vol_bytes = bytes;
     return SM_OK;
 }

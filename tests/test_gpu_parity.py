@@ -511,9 +511,10 @@ def test_capture_loop_replay(matcher, oracle, tmp_path):
         assert np.array_equal(np.asarray(Image.open(out / f"disp_{n}.png")), w), n
 
 
-@pytest.mark.parametrize("W,H,D", [(64, 16, 8), (333, 77, 100), (1920, 1080, 128), (5, 3, 7)])
+@pytest.mark.parametrize("W,H,D", [(64, 16, 8), (333, 77, 100), (1920, 1080, 128), (5, 3, 7), (3840, 5, 20)])
 def test_ad_volume(matcher, oracle, torch, W, H, D):
-    """PreCal / kernalPreCal_V2 (row a1) as a standalone HBM-bound kernel, bit-exact."""
+    """PreCal / kernalPreCal_V2 (row a1) as a standalone HBM-bound kernel, bit-exact (bands of rows per
+    block: 77 rows leave a partial last band, 3840 columns take 4 segments per thread)."""
     L, R = oracle.synth_pair(W + D, W, H, max(D, 16))
     want = oracle.precal(L, R, D)
     assert np.array_equal(matcher.ad_volume(L, R, D), want)

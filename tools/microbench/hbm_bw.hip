@@ -63,6 +63,48 @@ __global__ __launch_bounds__(256) void wrc(u32x4* __restrict__ p, size_t n) {
     }
 }
 
+// buffer-store variants (aux = cache policy bits: nt 2, sc0 1, sc1 16), grid-stride 16-B per lane
+template <int AUX>
+__global__ __launch_bounds__(256) void wrb(u32x4* __restrict__ p, size_t n) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1, 2};
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        // descriptor per 1 GiB-range chunk: 32-bit offsets cover 4 GiB
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(i * 16), 0, AUX);
+    }
+}
+// each wave writes KB consecutive KiB: store k at wave base + k KiB, lane 16 B apart
+template <int KB, bool NT>
+__global__ __launch_bounds__(256) void wrwave(u32x4* __restrict__ p, size_t n) {
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1, 2};
+    const size_t wave = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const size_t base = wave * 64 * KB + (threadIdx.x & 63);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        const size_t i = base + (size_t)k * 64;
+        if (i < n) {
+            if (NT) __builtin_nontemporal_store(v, p + i);
+            else p[i] = v;
+        }
+    }
+}
+// 32 B per lane (two adjacent 16-B stores), grid-stride
+template <bool NT>
+__global__ __launch_bounds__(256) void wr32(u32x4* __restrict__ p, size_t n) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1, 2};
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; 2 * i + 1 < n; i += stride) {
+        if (NT) {
+            __builtin_nontemporal_store(v, p + 2 * i);
+            __builtin_nontemporal_store(v, p + 2 * i + 1);
+        } else {
+            p[2 * i] = v;
+            p[2 * i + 1] = v;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void cp(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n) {
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride * 4) {
@@ -112,6 +154,25 @@ int main() {
                [&] { (void)hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0); });
         timeit("write 16B nt, 16384 blocks", bytes, [&] { wr<true><<<16384, 256>>>(b, n); });
         timeit("write 16B nt, 65536 blocks", bytes, [&] { wr<true><<<65536, 256>>>(b, n); });
+        timeit("write 16B chunk 4/lane nt", bytes, [&] { wrc<4, true><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        return 0;
+    }
+    if (getenv("HBM_W2")) {
+        timeit("hipMemsetAsync 1 GiB (write)", bytes, [&] { (void)hipMemsetAsync(b, 3, bytes, 0); });
+        timeit("write 16B nt, 65536 blocks", bytes, [&] { wr<true><<<65536, 256>>>(b, n); });
+        timeit("write 16B plain, 65536 blocks", bytes, [&] { wr<false><<<65536, 256>>>(b, n); });
+        timeit("buffer store aux 0, 65536 blocks", bytes, [&] { wrb<0><<<65536, 256>>>(b, n); });
+        timeit("buffer store nt, 65536 blocks", bytes, [&] { wrb<2><<<65536, 256>>>(b, n); });
+        timeit("buffer store sc1, 65536 blocks", bytes, [&] { wrb<16><<<65536, 256>>>(b, n); });
+        timeit("buffer store sc0 sc1, 65536 blocks", bytes, [&] { wrb<17><<<65536, 256>>>(b, n); });
+        timeit("buffer store nt sc1, 65536 blocks", bytes, [&] { wrb<18><<<65536, 256>>>(b, n); });
+        timeit("buffer store nt sc0 sc1, 65536 blocks", bytes, [&] { wrb<19><<<65536, 256>>>(b, n); });
+        timeit("wave-contiguous 4 KiB nt", bytes, [&] { wrwave<4, true><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        timeit("wave-contiguous 4 KiB plain", bytes, [&] { wrwave<4, false><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
+        timeit("wave-contiguous 16 KiB nt", bytes, [&] { wrwave<16, true><<<(unsigned)(n / (256 * 16)), 256>>>(b, n); });
+        timeit("wave-contiguous 16 KiB plain", bytes, [&] { wrwave<16, false><<<(unsigned)(n / (256 * 16)), 256>>>(b, n); });
+        timeit("32 B per lane nt, 32768 blocks", bytes, [&] { wr32<true><<<32768, 256>>>(b, n); });
+        timeit("32 B per lane plain, 32768 blocks", bytes, [&] { wr32<false><<<32768, 256>>>(b, n); });
         timeit("write 16B chunk 4/lane nt", bytes, [&] { wrc<4, true><<<(unsigned)(n / (256 * 4)), 256>>>(b, n); });
         return 0;
     }
