@@ -27,6 +27,7 @@
 // The maps are bit-exact with the restated oracle (oracle/st_oracle.c).
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <thread>
 #include <vector>
@@ -732,8 +733,18 @@ hipError_t upload_wave_job(StWorkspace& ws, int k, size_t per, const std::vector
 
 // One filter launch over 1 or 2 jobs: the wave filter when every level fits its LDS buffers, else the
 // workgroup-per-disparity filter.
+// SM_ST_WAVE_FILTER=0 forces the workgroup filter (the path of trees wider than the wave filter's LDS,
+// which no bundled image reaches; tests/test_gpu_segtree.py runs it this way)
+bool wave_filter_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SM_ST_WAVE_FILTER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_filter(const FilterJobs& fj, const WaveJobs& wj, int njobs, int maxw, int D, int P, hipStream_t s) {
-    if (maxw <= kWaveMaxLevel) {
+    if (maxw <= kWaveMaxLevel && wave_filter_enabled()) {
         hipLaunchKernelGGL(st_filter_wave_kernel, dim3((unsigned)D, (unsigned)njobs), dim3(64),
                            (size_t)kStLvlOff + (size_t)(2 * wave_level_stride(maxw)) * sizeof(float), s, wj, P);
     } else {

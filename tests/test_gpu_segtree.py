@@ -8,6 +8,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -106,3 +107,27 @@ def test_stmatch_cli(oracle, tmp_path, method):
     got = np.asarray(Image.open(op))
     want = (oracle.st2_disp if method else oracle.st_disp)(L, R, 48, 5, 0.1)[0]
     assert np.array_equal(got, want)
+
+
+def test_workgroup_filter_fallback():
+    """The workgroup-per-disparity filter (st_filter_kernel), which trees wider than the wave filter's
+    LDS buffers take, forced by SM_ST_WAVE_FILTER=0 in a child process: ST-1 and ST-2 bit-exact."""
+    import subprocess, sys, textwrap
+    code = textwrap.dedent("""
+        import sys, numpy as np
+        sys.path.insert(0, %r)
+        import gpu_stereo_matching_amd as sm
+        from oracle import oracle
+        rng = np.random.default_rng(21)
+        L = rng.integers(0, 256, (61, 97, 3), dtype=np.uint8)
+        L[:30, :32] = 77
+        R = np.roll(L, -5, axis=1)
+        with sm.BlockMatcher(0, 128, 64, 64) as m:
+            ok1 = np.array_equal(m.segment_tree(L, R, 16, 1, 0.1), oracle.st_disp(L, R, 16, 1, 0.1)[0])
+            ok2 = np.array_equal(m.segment_tree(L, R, 16, 1, 0.1, method=1), oracle.st2_disp(L, R, 16, 1, 0.1)[0])
+        print("OK" if ok1 and ok2 else "MISMATCH", ok1, ok2)
+    """ % ROOT)
+    env = dict(os.environ, SM_ST_WAVE_FILTER="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "OK" in out.stdout, out.stdout
