@@ -5,24 +5,26 @@
 //   guide + edge weights  GPU: 3x3 median of each BGR channel of the left view (MeanFilter(img, 1)
 //                         = ctmf, SegmentTree.cpp:185), max channel |diff| to the right / upper
 //                         neighbour (CColorWeight::GetWeight, :189-194)
-//   tree                  host: the reference builds it sequentially and so does this file.  Edges in
-//                         (weight, b, a) order (edge::operator<, SegmentTree.h:103-111) by a counting sort
-//                         over the 256 integer weights, filled in b order, which is that order exactly;
-//                         Kruskal with Felzenszwalb's size threshold, then the rest of the spanning tree
-//                         with the cross-segment penalty (segment-graph.h:48-101; disjoint-set.h:30-82);
-//                         neighbour lists in that edge order, BFS from pixel 0 (SegmentTree.cpp:71-130)
+//   edge order            GPU: the edges in (b, a) order, stably radix-sorted by weight, which is
+//                         edge::operator<'s (weight, b, a) order (SegmentTree.h:103-111); the sorted
+//                         edges come back to the host page-locked
+//   tree                  host: the reference builds it sequentially and so does this file: Kruskal with
+//                         Felzenszwalb's size threshold, then the rest of the spanning tree with the
+//                         cross-segment penalty (segment-graph.h:48-101; disjoint-set.h:30-82); neighbour
+//                         lists in the sorted edge order, BFS from pixel 0 (SegmentTree.cpp:71-130)
 //   cost volume           GPU: truncated colour + gradient cost (StereoHelper.cpp:37-129), written
 //                         channel-major in BFS order, C[d][i], so a tree level is a contiguous run
-//   filter                GPU: one workgroup per disparity d walks the BFS levels: leaf-to-root sums,
-//                         then root-to-leaf (SegmentTree.cpp:148-181), one barrier per level; each node
-//                         sums its children in the reference's order with separate multiplies and adds
+//   filter                GPU: one wave per disparity walks the BFS levels (st_filter_wave_kernel; one
+//                         workgroup per disparity for trees wider than its LDS): leaf-to-root sums, then
+//                         root-to-leaf (SegmentTree.cpp:148-181); each node sums its children in the
+//                         reference's order with separate multiplies and adds
 //   WTA, x scale, median  GPU: first d with the smallest cost (StereoHelper.cpp:131-154), times scale
 //                         (saturated; a non-decreasing map commutes with the median), then the 7x7
 //                         median (MeanFilter(disparity, 3), bm_post.hip)
 // ST-2 adds: the right view's cost taken from the left's (GetRightMatchingCostFromLeft,
 // StereoHelper.cpp:156-180: C_R(y, x, d) = C(y, min(x + d, W - 1), min(d, W - 1 - x)), computed directly),
 // a colour tree of each view filtered in one launch, the left-right check (bm_aux.hip), and a colour +
-// depth tree (CColorDepthWeight, SegmentTree.cpp:196-219) whose float weights the host forms from the
+// depth tree (CColorDepthWeight, SegmentTree.cpp:196-219) whose float weights the GPU forms from the
 // colour weights, the first left map and the mask, and orders by a stable radix sort of their bits.
 // The maps are bit-exact with the restated oracle (oracle/st_oracle.c).
 #include <algorithm>
@@ -237,8 +239,7 @@ struct WaveJob {
     const int* first;
     const uint32_t* child;
     const int4* task;          // [n_up tasks, leaf to root][n_dn tasks, root to leaf]
-    int n_up, n_dn;
-    int maxw;                  // widest level (sizes the LDS; the task records carry the offsets)
+    int n_up, n_dn;            // the task records carry the LDS offsets
     const float* table;
 };
 struct WaveJobs {
@@ -722,12 +723,12 @@ constexpr int kWaveMaxLevel = (65536 - kStLvlOff) / 8 - 64;   // 64 KB of LDS; w
 // Host task list `tv` of tree `d` into task slot k (`per` int4 each) of the workspace, which the caller
 // has grown for all its slots before the first upload; tv must stay alive until the copy has run.
 hipError_t upload_wave_job(StWorkspace& ws, int k, size_t per, const std::vector<int4>& tv, float* C, float* F,
-                           const DevTree& d, int n_up, int n_dn, int maxw, hipStream_t s, WaveJob& j) {
+                           const DevTree& d, int n_up, int n_dn, hipStream_t s, WaveJob& j) {
     if (tv.size() > per || ws.task_n < per * 4 * (size_t)(k + 1)) return hipErrorInvalidValue;
     int4* dst = reinterpret_cast<int4*>(ws.task) + per * (size_t)k;
     const hipError_t e = hipMemcpyAsync(dst, tv.data(), tv.size() * sizeof(int4), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
-    j = WaveJob{C, F, d.parent, d.pdist, d.first, d.child, dst, n_up, n_dn, maxw, d.table};
+    j = WaveJob{C, F, d.parent, d.pdist, d.first, d.child, dst, n_up, n_dn, d.table};
     return hipSuccess;
 }
 
@@ -834,7 +835,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     float* C = ws.vol;
     float* F = ws.vol + (size_t)P * D;
     WaveJobs wj{};
-    ST_CHK(upload_wave_job(ws, 0, tv.size(), tv, C, F, dt, n_up, n_dn, maxw, s, wj.j[0]));
+    ST_CHK(upload_wave_job(ws, 0, tv.size(), tv, C, F, dt, n_up, n_dn, s, wj.j[0]));
     hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
                        dt.rank, D, C);
     ST_CHK(hipGetLastError());
@@ -934,8 +935,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     const size_t per = std::max(tv0.size(), tv1.size());
     ST_CHK(grow(ws.task, ws.task_n, per * 4 * 2));
     WaveJobs wj{};
-    ST_CHK(upload_wave_job(ws, 0, per, tv0, C0, F0, d0, nu0, nd0, mw0, s, wj.j[0]));
-    ST_CHK(upload_wave_job(ws, 1, per, tv1, C1, F1, d1, nu1, nd1, mw1, s, wj.j[1]));
+    ST_CHK(upload_wave_job(ws, 0, per, tv0, C0, F0, d0, nu0, nd0, s, wj.j[0]));
+    ST_CHK(upload_wave_job(ws, 1, per, tv1, C1, F1, d1, nu1, nd1, s, wj.j[1]));
     ST_CHK(launch_filter(jobs, wj, 2, std::max(mw0, mw1), D, (int)P, s));
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, 1, raw0);
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F1, d1.rank, (int)P, D, 1, raw1);
@@ -966,7 +967,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     const int mw2 = wave_tasks(td, tv2, nu2, nd2);
     ST_CHK(grow(ws.task, ws.task_n, tv2.size() * 4));   // the first run's uploads completed at the sync above
     WaveJobs wj2{};
-    ST_CHK(upload_wave_job(ws, 0, tv2.size(), tv2, C0, F0, d0, nu2, nd2, mw2, s, wj2.j[0]));
+    ST_CHK(upload_wave_job(ws, 0, tv2.size(), tv2, C0, F0, d0, nu2, nd2, s, wj2.j[0]));
     ST_CHK(launch_filter(job2, wj2, 1, mw2, D, (int)P, s));
     hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, scale, raw0);
     ST_CHK(hipGetLastError());
