@@ -57,6 +57,17 @@ constexpr int kNB = kTileH / 16;   // 16-row CS hand-off blocks per tile
 constexpr int kPairs = 4;
 constexpr int kChunk = 2 * kPairs;
 constexpr int kCols = 64;
+// right-key partial rows: 16-B aligned groups of 4 u, reduced with 16-B loads (SM_RR_VEC=0: one
+// 4-B load per u and tile, the round-3 layout)
+#ifndef SM_RR_VEC
+#define SM_RR_VEC 1
+#endif
+constexpr bool kRrVec = SM_RR_VEC != 0;
+
+// pad slots in front of tile tx's partial row: lead + (u - tx*TW + dmax + 1) == 0 (mod 4) for u == 0 (mod 4)
+__host__ __device__ constexpr int rr_lead(int tx, int TW, int dmax) {
+    return kRrVec ? 1 + ((((tx * TW - dmax - 1) - 1) % 4 + 4) % 4) : 0;
+}
 
 template <int R, int DMAX, int NW = 4>
 struct Geo {
@@ -87,7 +98,10 @@ struct Geo {
     static constexpr int LDS_BYTES = FRONT + RS_BYTES;
     // fused right view (RIGHT kernels): per-tile right-key rows indexed by u - (x0 - DMAX - 1);
     // row stride == 1 (mod 64) keeps the 64 lanes of a scatter on distinct banks (2-way for NQ 14)
-    static constexpr int PW = TW + DMAX + 1;                    // partial row width written to HBM
+    static constexpr int PW = TW + DMAX + 1;                    // right-key entries per partial row
+    // partial row in HBM (SM_RR_VEC): the PW entries behind lead(tx) in 1..4 pad slots, so that the
+    // entry of every u = 0 (mod 4) is 16-B aligned in every tile's row; pads are neutral (0xFFFFFFFF)
+    static constexpr int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;
     static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
     static constexpr int RB_BYTES = kTileH * RBW * 4;
     static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
@@ -421,10 +435,11 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     }
     if constexpr (RIGHT) {
         // rb is untouched by the fold (which aliases the CS area); rows past H are never read
-        uint32_t* P = a.rpart + (int64_t)tile_id * (kTileH * G::PW);   // [frame][ty][tx][kTileH][PW]
-        for (int e = tid; e < kTileH * G::PW; e += kThreads) {
-            const int j = e / G::PW;
-            P[e] = rb[j * G::RBW + (e - j * G::PW)];
+        uint32_t* P = a.rpart + (int64_t)tile_id * (kTileH * G::PWP);   // [frame][ty][tx][kTileH][PWP]
+        const int lead = rr_lead(tx, G::TW, DMAX);
+        for (int e = tid; e < kTileH * G::PWP; e += kThreads) {
+            const int j = e / G::PWP, k = e - j * G::PWP - lead;
+            P[e] = (k >= 0 && k < G::PW) ? rb[j * G::RBW + k] : 0xFFFFFFFFu;
         }
     }
 }
@@ -476,6 +491,96 @@ __global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __
     }
 }
 
+// The same with the padded partial rows (SM_RR_VEC): a thread takes u = 4m..4m+3 and reads each covering
+// tile's four entries with one 16-B load.  The tile range is that of the group (a tile covering only some
+// of the four u holds 0xFFFFFFFF or a valid candidate of the others: every entry a tile writes is
+// C_L(u + d, d) of one of its pixels, so a min over a superset of the covering tiles is the same key).
+// The LR check then runs on 4 pixels per thread with dword loads and stores where the rows allow.
+template <int MAXT>
+__global__ __launch_bounds__(256) void right_reduce_lr_vec_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
+                                                                  int tiles_y, int TW, int PWP, int dmax, int d_hi,
+                                                                  int W, int H, int check, uint8_t* disp, int opitch,
+                                                                  int64_t ostride, uint8_t* __restrict__ right_out,
+                                                                  uint8_t* __restrict__ mask_out, int apitch,
+                                                                  int64_t astride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dr_row[];   // W rounded up to 4
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int ty = y / kTileH, j = y - ty * kTileH;
+    const uint32_t* base = rpart + (((int64_t)f * tiles_y + ty) * tiles_x * kTileH + j) * PWP;
+    const int64_t tstride = (int64_t)kTileH * PWP;
+    uint8_t* rrow = right_out ? right_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    const bool rvec = rrow && ((reinterpret_cast<uintptr_t>(rrow) & 3) == 0);
+    const int groups = (W + 3) >> 2;
+    for (int m = threadIdx.x; m < groups; m += blockDim.x) {
+        const int u = 4 * m;
+        const int tlo = u / TW;
+        const int thi = min(tiles_x - 1, (u + 3 + d_hi - 1) / TW);
+        uint4 v[MAXT];
+#pragma unroll
+        for (int k = 0; k < MAXT; ++k) {
+            const int tx = min(tlo + k, thi);   // repeated last tile: same keys, fixed trip count
+            const int idx = rr_lead(tx, TW, dmax) + u - tx * TW + dmax + 1;
+            v[k] = *reinterpret_cast<const uint4*>(base + tx * tstride + idx);
+        }
+        uint32_t k0 = v[0].x, k1 = v[0].y, k2 = v[0].z, k3 = v[0].w;
+#pragma unroll
+        for (int k = 1; k < MAXT; ++k) {
+            k0 = min(k0, v[k].x);
+            k1 = min(k1, v[k].y);
+            k2 = min(k2, v[k].z);
+            k3 = min(k3, v[k].w);
+        }
+        const uint32_t dr4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(k3, k2, 0x0C0C0400u),
+                                                   __builtin_amdgcn_perm(k1, k0, 0x0C0C0400u), 0x05040100u);
+        *reinterpret_cast<uint32_t*>(dr_row + u) = dr4;
+        if (rrow) {
+            if (rvec && u + 3 < W) {
+                *reinterpret_cast<uint32_t*>(rrow + u) = dr4;
+            } else {
+                for (int b = 0; b < 4 && u + b < W; ++b) rrow[u + b] = (uint8_t)(dr4 >> (8 * b));
+            }
+        }
+    }
+    if (!check) return;
+    __syncthreads();
+    uint8_t* drow = disp + (int64_t)f * ostride + (int64_t)y * opitch;
+    uint8_t* mrow = mask_out ? mask_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    const bool dvec = ((reinterpret_cast<uintptr_t>(drow) & 3) == 0) &&
+                      (!mrow || ((reinterpret_cast<uintptr_t>(mrow) & 3) == 0));
+    for (int m = threadIdx.x; m < groups; m += blockDim.x) {
+        const int x0 = 4 * m;
+        const bool vec = dvec && x0 + 3 < W;
+        uint32_t dw = 0;
+        if (vec) {
+            dw = *reinterpret_cast<const uint32_t*>(drow + x0);
+        } else {
+            for (int b = 0; b < 4 && x0 + b < W; ++b) dw |= (uint32_t)drow[x0 + b] << (8 * b);
+        }
+        uint32_t ow = 0, mw = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int x = x0 + b;
+            const int d = (dw >> (8 * b)) & 0xFF;
+            int occ = 1;
+            if (x - d >= 0) {
+                const int diff = d - (int)dr_row[x - d];
+                occ = (d == 0) || diff > 1 || diff < -1;
+            }
+            ow |= (uint32_t)(occ ? 0 : d) << (8 * b);
+            mw |= (uint32_t)(!occ) << (8 * b);
+        }
+        if (vec) {
+            *reinterpret_cast<uint32_t*>(drow + x0) = ow;
+            if (mrow) *reinterpret_cast<uint32_t*>(mrow + x0) = mw;
+        } else {
+            for (int b = 0; b < 4 && x0 + b < W; ++b) {
+                drow[x0 + b] = (uint8_t)(ow >> (8 * b));
+                if (mrow) mrow[x0 + b] = (uint8_t)(mw >> (8 * b));
+            }
+        }
+    }
+}
+
 // Output buffers of the fused right view (launch_box_match_lr).
 struct RightOut {
     int check;        // 1: apply the LR check to a.disp; 0: only produce dR
@@ -517,11 +622,20 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
                            (size_t)G::LDS_BYTES_R, s, a, tiles_x, tiles_y);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        // tiles covering one u: (TW + d_hi - 1) / TW + 1 at most
-        constexpr int kMaxT = (G::TW + DMAX - 1) / G::TW + 1;
-        hipLaunchKernelGGL((right_reduce_lr_kernel<kMaxT>), dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart,
-                           tiles_x, tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
-                           a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
+        if constexpr (kRrVec) {
+            // tiles covering one of u .. u + 3: ceil((d_hi + 2) / TW) + 1 at most
+            constexpr int kMaxT4 = (DMAX + 2 + G::TW - 1) / G::TW + 1;
+            hipLaunchKernelGGL((right_reduce_lr_vec_kernel<kMaxT4>), dim3(a.H, batch), dim3(256),
+                               (size_t)((a.W + 3) & ~3), s, a.rpart, tiles_x, tiles_y, G::TW, G::PWP, DMAX, a.d_hi,
+                               a.W, a.H, ro->check, a.disp, a.out_pitch, a.out_frame_stride, ro->right, ro->mask,
+                               ro->pitch, ro->stride);
+        } else {
+            // tiles covering one u: (TW + d_hi - 1) / TW + 1 at most
+            constexpr int kMaxT = (G::TW + DMAX - 1) / G::TW + 1;
+            hipLaunchKernelGGL((right_reduce_lr_kernel<kMaxT>), dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart,
+                               tiles_x, tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
+                               a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
+        }
     } else {
         // no more tiles than CUs (a small frame, batch 1): 16 waves per tile, >= 2 d-pairs each, so every
         // CU runs 16 waves instead of <= 4 (R <= 7: the wide-radius kernels need > 128 VGPRs).  Beyond
@@ -559,8 +673,9 @@ size_t partial_bytes_r(int W, int H, int D, int batch) {
     const int dmax = dspan <= 64 ? 64 : (dspan <= 128 ? 128 : (dspan <= 192 ? 192 : 256));
     const int TW = kCols - 2 * R;
     const int PW = TW + dmax + 1;
+    const int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;   // Geo::PWP
     const size_t tiles = (size_t)((W + TW - 1) / TW) * ((H + kTileH - 1) / kTileH);
-    return tiles * (size_t)batch * kTileH * PW * 4;
+    return tiles * (size_t)batch * kTileH * PWP * 4;
 }
 
 // ---------------------------------------------------------------------------------------
