@@ -262,13 +262,19 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 
 // r >= 6 needs > 168 VGPRs without spilling: 2 waves/SIMD there, 3 elsewhere; with the fused right
 // view r = 3 (7 outputs per S2H thread) spills at 168 and also runs at 2
-// SM_G_ROLES_RIGHT (A/B only): the wave roles in the right-view kernel too, at 2 waves/SIMD (its
-// registers do not fit 3 with them)
+// SM_G_ROLES_RIGHT: the phase-1 wave roles in the right-view kernel too.  2 (default): at r = 0, 1, 4, 5,
+// where the kernel keeps 3 waves/SIMD with them (<= 168 VGPRs: the output guide values packed as f16
+// pairs and one validity register, kLeanS2H); 1 (A/B only): every radius, at 2 waves/SIMD; 0: never.
+// Same box, guided + LR, 1080p D=128 32 frames per call, us per frame: r = 5 549.1 -> 523.0, r = 4
+// 532.7 -> 518.9, r = 1 373.0 -> 368.4; 4K D=192 8 frames, r = 5: 3238 -> 3083; maps bit-identical.
+// 1 ran 552 -> 650 (round 3, 2 waves/SIMD)
 #ifndef SM_G_ROLES_RIGHT
-#define SM_G_ROLES_RIGHT 0
+#define SM_G_ROLES_RIGHT 2
 #endif
+template <int R>
+constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && (R <= 1 || R == 4 || R == 5));
 template <int R, bool RIGHT>
-constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT))) ? 2 : 3;
+constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
 // right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
 constexpr float kRightScale = 16384.0f;
@@ -280,9 +286,14 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
-    // wave roles without the fused right view only: its key chain leaves no registers for the taller
-    // strips (168-VGPR budget, spills measured in the ISA)
-    constexpr bool ROLES = kGuidedRoles && (!RIGHT || SM_G_ROLES_RIGHT);
+    // wave roles with the fused right view only where its key chain leaves registers for the taller
+    // strips at 3 waves/SIMD (kRolesRight: r = 0, 1, 4, 5 with the LEAN state below)
+    constexpr bool ROLES = kGuidedRoles && (!RIGHT || kRolesRight<R>);
+    // the right view with the roles needs S2H's per-output state in fewer registers: I as f16 pairs read
+    // by v_fma_mix_f32 (the same single-rounding fma, so the same maps; issued as VOP3P it costs more than
+    // the v_fmac the f32 form gets: +0.8 % on the left-only kernel, which keeps that form; at r = 2 the
+    // right view measured 409.6 -> 417.5 us/frame with it instead of its 5 spilled VGPRs, not kept)
+    constexpr bool LEAN = RIGHT && ROLES;
     using G = GeoF<R, ROLES>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
@@ -382,8 +393,15 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     uint32_t nN[G::SW1];
     uint32_t nSI[G::SW1];
     float fSI[G::SW1], invden[G::SW1], invN[G::SW1];
-    float oI[G::SW2], bq[G::SW2];
-    int bdd[G::SW2], dlim[G::SW2];
+    // output guide values I: f32, or (LEAN) f16 pairs, exact for 0..255
+    float oI[LEAN ? 1 : G::SW2];
+    uint32_t oIh[LEAN ? (G::SW2 + 1) / 2 : 1];
+    float bq[G::SW2];
+    int bdd[G::SW2], dlim[LEAN ? 1 : G::SW2];
+    // LEAN: the validity d <= W - x (Device.cu:44; mirrored pass: d <= x) as d - dsgn * o <= dl0 for
+    // output o, one VGPR instead of one per output (the left-hand side is wave-uniform)
+    const int dsgn = valid_mode != 1 ? -1 : 1;
+    const int dl0 = valid_mode != 1 ? W - (x0 + h2s * G::SW2) : x0 + h2s * G::SW2;
     // fused right view: 2^14 / N per output (NaN for outputs outside the image or the tile, whose
     // keys then clamp to the maximum), and the key slots
     float rinv[RIGHT ? G::SW2 : 1];
@@ -392,10 +410,16 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     for (int o = 0; o < G::SW2; ++o) {
         const int x = x0 + h2s * G::SW2 + o;
         const bool ok = oy < H && x < W && h2s * G::SW2 + o < G::TW;
-        oI[o] = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
+        const float iv = ok ? (float)L[(int64_t)oy * pitch + x] : 0.f;
+        if constexpr (LEAN) {
+            const uint32_t ih = __builtin_bit_cast(uint16_t, (_Float16)iv);
+            oIh[o / 2] = (o % 2 == 0) ? ih : (oIh[o / 2] | (ih << 16));
+        } else {
+            oI[o] = iv;
+            dlim[o] = valid_mode != 1 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
+        }
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
-        dlim[o] = valid_mode != 1 ? (W - x) : x;   // d <= W - x (Device.cu:44); mirrored pass: d <= x
         if constexpr (RIGHT) {
             rinv[o] = ok ? kRightScale / (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_nanf("");
             rk[o] = INT_MAX;
@@ -527,8 +551,8 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         // also loads the 2R warm-up rows), before its mm stores, as in S1H; a row's registers are
         // free once no later group reads it.  Each group restarts its running sums from its own 2R
         // warm-up rows, as an 8-row strip does without the roles: the float sums, and so the maps, are
-        // the same bit for bit in every configuration (the right-view kernel runs without the roles,
-        // and the LR check pairs its left map with the left-only kernel's)
+        // the same bit for bit in every configuration (the right-view kernel runs without the roles at
+        // r = 2, 3, 6, 7, and the LR check pairs its left map with the left-only kernel's)
         constexpr int NRW = G::RPS + 2 * R;
         float2 v[NRW];
 #pragma unroll
@@ -562,7 +586,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         }
     };
     // ================= S2H + WTA =================
-    // LIM: some output of the tile can have d > its dlim (tile-uniform; interior tiles skip the test)
+    // LIM: some output of the tile can have d past its validity limit (tile-uniform; interior tiles skip the test)
     auto s2h = [&](int d, auto lim) {
         constexpr bool LIM = decltype(lim)::value;
         constexpr int NR = G::SW2 + 2 * R;   // mm values read per plane
@@ -588,8 +612,20 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         for (int o = 0; o < G::SW2; ++o) {
             sa += va[o + 2 * R];
             sb += vb[o + 2 * R];
-            const float q = sa * oI[o] + sb;
-            const bool take = (!LIM || d <= dlim[o]) && q < bq[o];
+            float q;   // sa * I + sb, one rounding
+            bool valid;
+            if constexpr (LEAN) {
+                if (o % 2 == 0)
+                    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(q) : "v"(sa), "v"(oIh[o / 2]), "v"(sb));
+                else
+                    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]"
+                        : "=v"(q) : "v"(sa), "v"(oIh[o / 2]), "v"(sb));
+                valid = d - dsgn * o <= dl0;
+            } else {
+                q = sa * oI[o] + sb;
+                valid = d <= dlim[o];
+            }
+            const bool take = (!LIM || valid) && q < bq[o];
             bq[o] = take ? q : bq[o];
             bdd[o] = take ? d : bdd[o];
             if constexpr (RIGHT) {
@@ -726,7 +762,7 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     if (blocks <= 0 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // the left-only kernel may run the phase-1 wave roles: its LDS plan is GeoF<R, kGuidedRoles>'s
     constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS;
-    constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && SM_G_ROLES_RIGHT>::LDS;
+    constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && kRolesRight<R>>::LDS;
     if (!gpart) {
         hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), lds_left, s, L,
                            Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
