@@ -287,7 +287,20 @@ def run_variants(sm, torch, dev, stream, seed):
             out[name + " (sm_host_alloc buffers)"] = {
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
                 "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
-            del Lp, Rp, Op
+            # the pair in one page-locked block (right frame after the left one): one upload copy
+            pair = sm.host_empty((2, H, W))
+            pair[0], pair[1] = L, R
+            for _ in range(3):
+                m.match(pair[0], pair[1], r, D, out=Op)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                m.match(pair[0], pair[1], r, D, out=Op)
+            ms = (time.perf_counter() - t0) * 1000 / n
+            up, mt, dn = m.stage_ms()
+            out[name + " (sm_host_alloc, pair in one block)"] = {
+                "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
+                "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+            del Lp, Rp, Op, pair
         # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's
         # defaults: a synchronous host call (host tree builds + GPU cost / filter / WTA / median / LR check), wall
         g = np.load(os.path.join(ROOT, "tests", "golden", "middlebury_bgr.npz"))

@@ -394,6 +394,15 @@ bool zero_copy_enabled() {
     return on;
 }
 
+// SM_PAIR_COPY=0 (A/B only): a contiguous host pair still goes up as two copies
+bool pair_copy_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SM_PAIR_COPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Host-pointer pass over one frame (or one row band of a frame: sm_group_*).  Only result rows
 // [keep0, keep1) are downloaded, into disp_out / right_out / mask_out pointing at row keep0.
 int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
@@ -438,10 +447,19 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
     if (zero_copy_enabled() && keep0 == 0 && keep1 == height && !right_out && !mask_out && !(flags & SM_LR_CHECK))
         mapped = host_block_device_ptr(disp_out, (size_t)(height - 1) * out_pitch + width);
     SM_HIP(hipEventRecord(h->ev[0], s));
-    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
-    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    // a pair with the right frame right after the left one (one sm_host_alloc block of 2 frames, or any
+    // contiguous (2, H, W) array) goes up as one copy into d_left .. d_left + 2P: one DMA transfer
+    // instead of two
+    uint8_t* dR = h->d_right;
+    if (pitch == width && right == left + P && pair_copy_enabled()) {
+        dR = h->d_left + P;
+        SM_HIP(hipMemcpyAsync(h->d_left, left, (size_t)(2 * P), hipMemcpyHostToDevice, s));
+    } else {
+        SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+        SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    }
     SM_HIP(hipEventRecord(h->ev[1], s));
-    rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags,
+    rc = run_device(h, h->d_left, dR, width, height, width, 1, P, radius, num_disp, flags,
                     mapped ? mapped : h->d_disp, mapped ? out_pitch : width, P, right_out ? aux : nullptr,
                     mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
@@ -842,8 +860,10 @@ SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm
     h->max_d = max_disp;
     const size_t P = (size_t)max_width * max_height;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&h->d_left, P);
-    if (e == hipSuccess) e = hipMalloc(&h->d_right, P);
+    // the pair's device frames are one allocation (d_right = d_left + P), so a host pair that sits in one
+    // block (right frame right after the left one) uploads as one DMA copy
+    if (e == hipSuccess) e = hipMalloc(&h->d_left, 2 * P);
+    if (e == hipSuccess) h->d_right = h->d_left + P;
     if (e == hipSuccess) e = hipMalloc(&h->d_disp, P);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming);
@@ -861,8 +881,7 @@ SM_API int sm_destroy(sm_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->scratch_ev && h->scratch_pending) (void)hipEventSynchronize(h->scratch_ev);   // device calls on other streams
-    (void)hipFree(h->d_left);
-    (void)hipFree(h->d_right);
+    (void)hipFree(h->d_left);   // d_right lies in the same allocation
     (void)hipFree(h->d_disp);
     (void)hipFree(h->d_lr);
     (void)hipFree(h->d_rpart);

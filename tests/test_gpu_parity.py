@@ -632,6 +632,28 @@ def test_pinned_host_buffers(sm, matcher, oracle):
     assert np.array_equal(chk, chk_o) and np.array_equal(rd, rd_o) and np.array_equal(mask, mask_o)
 
 
+@pytest.mark.parametrize("W,H,D,r", [(1920, 1080, 128, 5), (463, 370, 64, 4), (97, 31, 40, 0), (333, 150, 64, 11)])
+def test_pair_in_one_block(sm, matcher, oracle, W, H, D, r):
+    """A pair whose right frame follows the left one in memory (one (2, H, W) block: page-locked from
+    sm_host_alloc, or a pageable numpy array) goes up as one copy; maps bit-exact with the oracle for
+    box, box + LR and guided, and the next call on separate frames is unaffected."""
+    L, R = oracle.synth_pair(60 + r, W, H, D)
+    want = oracle.box_disp(L, R, r, D)
+    _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, r, D)
+    for pair in (sm.host_empty((2, H, W)), np.empty((2, H, W), np.uint8)):
+        pair[0], pair[1] = L, R
+        assert pair[1].ctypes.data == pair[0].ctypes.data + W * H
+        assert np.array_equal(matcher.match(pair[0], pair[1], r, D), want)
+        Op = sm.host_empty((H, W))
+        assert np.array_equal(matcher.match(pair[0], pair[1], r, D, out=Op), want)
+        chk, rd, mask = matcher.match_lr(pair[0], pair[1], r, D)
+        assert np.array_equal(chk, chk_o) and np.array_equal(rd, rd_o) and np.array_equal(mask, mask_o)
+        if r <= 7:
+            g_pair = matcher.match(pair[0], pair[1], r, D, agg="guided")
+            assert np.array_equal(g_pair, matcher.match(L.copy(), R.copy(), r, D, agg="guided"))
+    assert np.array_equal(matcher.match(L, R, r, D), want)
+
+
 @pytest.mark.parametrize("agg,med", [("box", False), ("box", True), ("guided", False), ("box-staged", False),
                                      ("box-staged", True)])
 def test_zero_copy_map(sm, matcher, oracle, agg, med):

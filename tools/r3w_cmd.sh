@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r3w_pytest_gpu.txt 2>&1; rc=$?; tail -3 gpurun_out/r3w_pytest_gpu.txt; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r3w_pytest_gpu.txt | head; exit $rc; }
+timeout -k 10 300 python tools/roundtrip_ab.py > gpurun_out/r3w_rt.txt 2>&1; cat gpurun_out/r3w_rt.txt | tail -20
+timeout -k 10 300 python bench.py > gpurun_out/r3w_bench.json 2> gpurun_out/r3w_bench.err && python -c "
+import json; d=json.load(open('gpurun_out/r3w_bench.json'))
+for k,v in d['variants'].items():
+    if 'round trip' in k: print(k, v)"

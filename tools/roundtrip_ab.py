@@ -10,7 +10,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     W, H, D, r = 1920, 1080, 128, 5
     L, R = sm.synth_pair(1234, W, H, D)
     with sm.BlockMatcher(0, W, H, 256) as m:
-        Lp, Rp, Op = sm.host_empty((H, W)), sm.host_empty((H, W)), sm.host_empty((H, W))
+        Op = sm.host_empty((H, W))
+        if os.environ.get("SM_AB_PAIR") == "1":   # the pair in one page-locked block
+            pair = sm.host_empty((2, H, W))
+            Lp, Rp = pair[0], pair[1]
+        else:
+            Lp, Rp = sm.host_empty((H, W)), sm.host_empty((H, W))
         Lp[...] = L
         Rp[...] = R
         for _ in range(20):
@@ -22,7 +27,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
             ts.append(time.perf_counter() - t0)
         print("RESULT", statistics.median(ts) * 1e3, *m.stage_ms())
     sys.exit(0)
-SETTINGS = {"dma": {"SM_ZERO_COPY": "0"}, "zc": {"SM_ZERO_COPY": "1"}}
+SETTINGS = {"dma": {"SM_ZERO_COPY": "0"}, "zc": {"SM_ZERO_COPY": "1"},
+            # round 3: the pair in one block, uploaded as one copy (default) or as two (SM_PAIR_COPY=0)
+            "zc_pair": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1"},
+            "zc_pair_2copies": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_PAIR_COPY": "0"}}
 res = {k: [] for k in SETTINGS}
 for _ in range(3):
     for zc, env in SETTINGS.items():
@@ -33,7 +41,8 @@ for _ in range(3):
             print(out.stdout, out.stderr)
             sys.exit(1)
         res[zc].append([float(v) for v in line[0].split()[1:]])
-for zc, name in (("dma", "DMA up + download"), ("zc", "DMA up + zero-copy map")):
+for zc, name in (("dma", "DMA up + download"), ("zc", "DMA up + zero-copy map"),
+                 ("zc_pair", "pair block, one copy + zc map"), ("zc_pair_2copies", "pair block, two copies + zc")):
     walls = [v[0] for v in res[zc]]
     print(f"{name:28s} wall ms/call median {statistics.median(walls):.4f} all {[round(w, 4) for w in walls]} "
           f"last stages upload/match/download {[round(x, 4) for x in res[zc][-1][1:]]}")
