@@ -300,6 +300,17 @@ def run_variants(sm, torch, dev, stream, seed):
             out[name + " (sm_host_alloc, pair in one block)"] = {
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
                 "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+            # the same without the stage-split events (SM_PARAM_STAGE_TIMING 0): the drop-in call's wall
+            m.set_stage_timing(False)
+            for _ in range(3):
+                m.match(pair[0], pair[1], r, D, out=Op)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                m.match(pair[0], pair[1], r, D, out=Op)
+            ms = (time.perf_counter() - t0) * 1000 / n
+            m.set_stage_timing(True)
+            out[name + " (sm_host_alloc, pair in one block, no stage timing)"] = {
+                "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1}
             del Lp, Rp, Op, pair
         # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's
         # defaults: a synchronous host call (host tree builds + GPU cost / filter / WTA / median / LR check), wall

@@ -26,6 +26,7 @@ SM_STAGED = 8
 
 SM_PARAM_GUIDED_EPS = 1
 SM_PARAM_STAGED_GROUP = 2
+SM_PARAM_STAGE_TIMING = 3
 
 # every symbol include/sm_hip.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = (

@@ -59,6 +59,7 @@ struct sm_handle {
     size_t bgr_bytes = 0;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
     int staged_group = 8;        // SM_STAGED frames per launch group (SM_PARAM_STAGED_GROUP)
+    bool stage_timing = true;    // host calls record the upload / match / download split (SM_PARAM_STAGE_TIMING)
     // The workspaces above are shared by every call on the handle while calls run on the stream
     // they are given: the end of each pass is recorded here, and a pass on another stream waits
     // for it first, so two streams never write the same workspace at once.
@@ -458,12 +459,15 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
         SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
         SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     }
-    SM_HIP(hipEventRecord(h->ev[1], s));
+    // stage split events (SM_PARAM_STAGE_TIMING): each costs a marker between the copy and compute
+    // queues, ~10 us per 1080p call for the two (profiles/microbench/r03_roundtrip_pair_block.txt)
+    const bool ev = h->stage_timing;
+    if (ev) SM_HIP(hipEventRecord(h->ev[1], s));
     rc = run_device(h, h->d_left, dR, width, height, width, 1, P, radius, num_disp, flags,
                     mapped ? mapped : h->d_disp, mapped ? out_pitch : width, P, right_out ? aux : nullptr,
                     mask_out ? aux + P : nullptr, width, P, s);
     if (rc) return rc;
-    SM_HIP(hipEventRecord(h->ev[2], s));
+    if (ev) SM_HIP(hipEventRecord(h->ev[2], s));
     const int64_t k0 = (int64_t)keep0 * width;
     const int nk = keep1 - keep0;
     if (!mapped) SM_HIP(copy2d(disp_out, out_pitch, h->d_disp + k0, width, width, nk, hipMemcpyDeviceToHost, s));
@@ -471,9 +475,13 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
     if (mask_out) SM_HIP(copy2d(mask_out, out_pitch, aux + P + k0, width, width, nk, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
     SM_HIP(hipEventSynchronize(h->ev[3]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    if (ev) {
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    } else {
+        h->stage_ms[0] = h->stage_ms[1] = h->stage_ms[2] = 0.f;
+    }
     return SM_OK;
 }
 
@@ -912,6 +920,11 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
         if ((float)g != value || g < 1 || g > kStagedGroup)
             return fail(SM_ERR_INVALID_ARG, "staged launch group must be an integer in [1, %d]", kStagedGroup);
         h->staged_group = g;
+        return SM_OK;
+    }
+    if (param == SM_PARAM_STAGE_TIMING) {
+        if (value != 0.f && value != 1.f) return fail(SM_ERR_INVALID_ARG, "stage timing is 0 or 1");
+        h->stage_timing = value != 0.f;
         return SM_OK;
     }
 

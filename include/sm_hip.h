@@ -63,8 +63,11 @@ enum {
 /* ---- scalar parameters (sm_set_param_f) ---- */
 enum {
     SM_PARAM_GUIDED_EPS = 1,  /* guided-filter epsilon in AD^2 units (default 6.5025 = 1e-4 * 255^2) */
-    SM_PARAM_STAGED_GROUP = 2 /* SM_STAGED frames per launch group, 1..8 (default 8): bounds the
-                                 handle's staged workspace (see SM_STAGED) */
+    SM_PARAM_STAGED_GROUP = 2, /* SM_STAGED frames per launch group, 1..8 (default 8): bounds the
+                                  handle's staged workspace (see SM_STAGED) */
+    SM_PARAM_STAGE_TIMING = 3  /* 1 (default): host calls record the upload / match / download split
+                                  read by sm_last_stage_ms; 0: they skip those hipEvents (~10 us less
+                                  per 1080p call) and sm_last_stage_ms reports 0 */
 };
 
 typedef struct sm_handle sm_handle;

@@ -384,10 +384,21 @@ def test_error_codes_side_entries(sm, torch):
     small.close()
 
 
-def test_stage_timings(matcher, gray):
-    matcher.match(gray["Art_/view1"], gray["Art_/view5"], 5, 64)
+def test_stage_timings(matcher, gray, oracle):
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    want = matcher.match(L, R, 5, 64)
     u, c, d = matcher.stage_ms()
     assert u > 0 and c > 0 and d > 0
+    # SM_PARAM_STAGE_TIMING 0: no stage events, the split reads 0, the map is unchanged
+    matcher.set_stage_timing(False)
+    try:
+        assert np.array_equal(matcher.match(L, R, 5, 64), want)
+        assert matcher.stage_ms() == (0.0, 0.0, 0.0)
+    finally:
+        matcher.set_stage_timing(True)
+    matcher.match(L, R, 5, 64)
+    assert min(matcher.stage_ms()) > 0
+    assert np.array_equal(want, oracle.box_disp(L, R, 5, 64))
 
 
 def test_frame_stream_pipeline(matcher, oracle, torch):

@@ -11,6 +11,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     L, R = sm.synth_pair(1234, W, H, D)
     with sm.BlockMatcher(0, W, H, 256) as m:
         Op = sm.host_empty((H, W))
+        if os.environ.get("SM_AB_NOTIMING") == "1":   # no stage-split events (SM_PARAM_STAGE_TIMING 0)
+            m.set_stage_timing(False)
         if os.environ.get("SM_AB_PAIR") == "1":   # the pair in one page-locked block
             pair = sm.host_empty((2, H, W))
             Lp, Rp = pair[0], pair[1]
@@ -30,7 +32,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
 SETTINGS = {"dma": {"SM_ZERO_COPY": "0"}, "zc": {"SM_ZERO_COPY": "1"},
             # round 3: the pair in one block, uploaded as one copy (default) or as two (SM_PAIR_COPY=0)
             "zc_pair": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1"},
-            "zc_pair_2copies": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_PAIR_COPY": "0"}}
+            "zc_pair_2copies": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_PAIR_COPY": "0"},
+            "zc_pair_noev": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_AB_NOTIMING": "1"}}
 res = {k: [] for k in SETTINGS}
 for _ in range(3):
     for zc, env in SETTINGS.items():
@@ -42,7 +45,8 @@ for _ in range(3):
             sys.exit(1)
         res[zc].append([float(v) for v in line[0].split()[1:]])
 for zc, name in (("dma", "DMA up + download"), ("zc", "DMA up + zero-copy map"),
-                 ("zc_pair", "pair block, one copy + zc map"), ("zc_pair_2copies", "pair block, two copies + zc")):
+                 ("zc_pair", "pair block, one copy + zc map"), ("zc_pair_2copies", "pair block, two copies + zc"),
+                 ("zc_pair_noev", "pair block, one copy, no stage events")):
     walls = [v[0] for v in res[zc]]
     print(f"{name:28s} wall ms/call median {statistics.median(walls):.4f} all {[round(w, 4) for w in walls]} "
           f"last stages upload/match/download {[round(x, 4) for x in res[zc][-1][1:]]}")
