@@ -452,7 +452,8 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
     // contiguous (2, H, W) array) goes up as one copy into d_left .. d_left + 2P: one DMA transfer
     // instead of two
     uint8_t* dR = h->d_right;
-    if (pitch == width && right == left + P && pair_copy_enabled()) {
+    if (pitch == width && reinterpret_cast<uintptr_t>(right) == reinterpret_cast<uintptr_t>(left) + (uintptr_t)P &&
+        pair_copy_enabled()) {
         dR = h->d_left + P;
         SM_HIP(hipMemcpyAsync(h->d_left, left, (size_t)(2 * P), hipMemcpyHostToDevice, s));
     } else {
