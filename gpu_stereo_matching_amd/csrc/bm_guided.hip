@@ -264,7 +264,9 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 // view r = 3 (7 outputs per S2H thread) spills at 168 and also runs at 2
 // SM_G_ROLES_RIGHT: the phase-1 wave roles in the right-view kernel too.  2 (default): at r = 0, 1, 4, 5,
 // where the kernel keeps 3 waves/SIMD with them (<= 168 VGPRs: the output guide values packed as f16
-// pairs and one validity register, kLeanS2H); 1 (A/B only): every radius, at 2 waves/SIMD; 0: never.
+// pairs and one validity register, LEAN below), and at r = 3, whose right view runs 2 waves/SIMD either
+// way (598.4 vs 618.8 us per 1080p frame); not at r = 2 (spills at 3 waves/SIMD); 1 (A/B only): every
+// radius, at 2 waves/SIMD; 0: never.
 // Same box, guided + LR, 1080p D=128 32 frames per call, us per frame: r = 5 549.1 -> 523.0, r = 4
 // 532.7 -> 518.9, r = 1 373.0 -> 368.4; 4K D=192 8 frames, r = 5: 3238 -> 3083; maps bit-identical.
 // 1 ran 552 -> 650 (round 3, 2 waves/SIMD)
@@ -272,7 +274,7 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 #define SM_G_ROLES_RIGHT 2
 #endif
 template <int R>
-constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && (R <= 1 || R == 4 || R == 5));
+constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && R <= 5 && R != 2);
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
     // wave roles with the fused right view only where its key chain leaves registers for the taller
-    // strips at 3 waves/SIMD (kRolesRight: r = 0, 1, 4, 5 with the LEAN state below)
+    // strips (kRolesRight: r = 0, 1, 4, 5 at 3 waves/SIMD with the LEAN state below, r = 3 at 2)
     constexpr bool ROLES = kGuidedRoles && (!RIGHT || kRolesRight<R>);
     // the right view with the roles needs S2H's per-output state in fewer registers: I as f16 pairs read
     // by v_fma_mix_f32 (the same single-rounding fma, so the same maps; issued as VOP3P it costs more than
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         // free once no later group reads it.  Each group restarts its running sums from its own 2R
         // warm-up rows, as an 8-row strip does without the roles: the float sums, and so the maps, are
         // the same bit for bit in every configuration (the right-view kernel runs without the roles at
-        // r = 2, 3, 6, 7, and the LR check pairs its left map with the left-only kernel's)
+        // r = 2, 6, 7, and the LR check pairs its left map with the left-only kernel's)
         constexpr int NRW = G::RPS + 2 * R;
         float2 v[NRW];
 #pragma unroll

@@ -85,8 +85,8 @@ def _check_guided_lr(matcher, oracle, L, R, r, D, min_exact=0.99):
 
 @pytest.mark.parametrize("r,D", [(5, 64), (3, 48), (0, 16), (7, 32), (1, 100), (4, 80), (2, 40)])
 def test_guided_lr_art(matcher, oracle, gray, r, D):
-    """Every right-view build: with the phase-1 wave roles (r = 0, 1, 4, 5, kRolesRight) and without
-    (r = 2, 3, 7)."""
+    """Every right-view build: with the phase-1 wave roles (r = 0, 1, 3, 4, 5, kRolesRight) and without
+    (r = 2, 7)."""
     L, R = gray["Art_/view1"], gray["Art_/view5"]
     mask = _check_guided_lr(matcher, oracle, L, R, r, D)
     assert 0.3 < mask.mean() < 1.0
