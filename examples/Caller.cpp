@@ -112,9 +112,11 @@ void cvtColorTest() {
     write_pgm(env_or("SM_OUT", "gray.pgm"), gray);
 }
 
-// Not a reference demo: BlockMatching.h's testBM / getDisp / PreCal through the adapter (the
-// reference uses them to cross-check its GPU path, BlockMatching.cpp:263-308).  Writes the
-// testBM and getDisp maps (PGM) and the AD volume (raw, D planes).
+// Not a reference demo: all seven BlockMatching.h functions through the adapter (the reference uses
+// them to cross-check its GPU path, Device.cu:241-243, 265-268, 297; BlockMatching.cpp:263-308).
+// Writes the testBM and getDisp maps (PGM), the AD volume (raw, D planes) and the getAllSAD volume
+// (raw, pixel-major), then runs compareDiff / compareDisp / compareSAD on the results as computed
+// and once more with one planted mismatch each (stdout sections "== compareX clean|planted").
 void blockMatchingApiTest() {
     sm::Mat g1, g2, disp;
     if (!read_pgm(env_or("SM_LEFT", "view1_.pgm"), g1) || !read_pgm(env_or("SM_RIGHT", "view5_.pgm"), g2)) {
@@ -123,13 +125,39 @@ void blockMatchingApiTest() {
     }
     const int sad = std::atoi(env_or("SM_SAD", "5").c_str());
     const int range = std::atoi(env_or("SM_RANGE", "64").c_str());
+    const int rows = g1.rows, cols = g1.cols, total = rows * cols;
     testBM(g1, g2, disp, sad, range);
     write_pgm(env_or("SM_OUT", "disp.pgm"), disp);
-    sm::Mat disp2(g1.rows, g1.cols);
+    sm::Mat disp2(rows, cols);
     getDisp(g1, g2, disp2.data, sad, range);
     write_pgm(env_or("SM_OUT2", "disp2.pgm"), disp2);
-    std::vector<uchar> dif((size_t)g1.rows * g1.cols * range, 0);
+    std::vector<uchar> dif((size_t)total * range, 0);
     PreCal(g1, g2, dif.data(), sad, range);
-    std::ofstream f(env_or("SM_VOL", "dif.u8"), std::ios::binary);
-    f.write(reinterpret_cast<const char*>(dif.data()), (std::streamsize)dif.size());
+    {
+        std::ofstream f(env_or("SM_VOL", "dif.u8"), std::ios::binary);
+        f.write(reinterpret_cast<const char*>(dif.data()), (std::streamsize)dif.size());
+    }
+    std::vector<uchar> all((size_t)total * range, 0);
+    getAllSAD(g1, g2, all.data(), sad, range);
+    {
+        std::ofstream f(env_or("SM_SADVOL", "allsad.u8"), std::ios::binary);
+        f.write(reinterpret_cast<const char*>(all.data()), (std::streamsize)all.size());
+    }
+    std::cout << "== compareDiff clean" << std::endl;
+    compareDiff(g1, g2, dif.data(), sad, range, total);
+    std::cout << std::endl << "== compareDisp clean" << std::endl;
+    compareDisp(g1, g2, disp2.data, sad, range, cols, rows);
+    std::cout << "== compareSAD clean" << std::endl;
+    compareSAD(g1, g2, all.data(), sad, range, cols, rows);
+    std::cout << std::endl;
+    dif[7] ^= 1;
+    disp2.data[1 * cols + 2] ^= 1;
+    all[5] ^= 1;
+    std::cout << "== compareDiff planted" << std::endl;
+    compareDiff(g1, g2, dif.data(), sad, range, total);
+    std::cout << std::endl << "== compareDisp planted" << std::endl;
+    compareDisp(g1, g2, disp2.data, sad, range, cols, rows);
+    std::cout << "== compareSAD planted" << std::endl;
+    compareSAD(g1, g2, all.data(), sad, range, cols, rows);
+    std::cout << std::endl;
 }

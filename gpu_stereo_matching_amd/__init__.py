@@ -257,6 +257,28 @@ class BlockMatcher:
                                               out.ctypes.data))
         return out
 
+    def all_sad(self, left, right, radius: int, num_disp: int) -> np.ndarray:
+        """getAllSAD (BlockMatching.cpp:191-261) on the GPU: uint8 [H, W, num_disp] (pixel-major
+        ``data_dm[p * D + d]``), each window SAD truncated to uchar, 255 where x + d > W."""
+        L = _as_u8_image(left, "left")
+        R = _as_u8_image(right, "right")
+        H, W = L.shape
+        out = np.empty((H, W, num_disp), np.uint8)
+        _capi.check(self._lib.sm_all_sad_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
+                                            out.ctypes.data))
+        return out
+
+    def all_sad_device(self, left_t, right_t, radius: int, num_disp: int, out_t=None, stream=None):
+        """Device form of :meth:`all_sad`: uint8 [H, W, num_disp] CUDA tensor, async on `stream`."""
+        import torch
+        H, W = left_t.shape
+        if out_t is None:
+            out_t = torch.empty((H, W, num_disp), dtype=torch.uint8, device=left_t.device)
+        _check_out(out_t, (H, W, num_disp), torch.uint8, left_t.device)
+        _capi.check(self._lib.sm_all_sad_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, radius,
+                                                num_disp, out_t.data_ptr(), self._stream_ptr(stream)))
+        return out_t
+
     def sad_volume_device(self, left_t, right_t, radius: int, num_disp: int, out_t=None, stream=None):
         """u16 SAD volume [num_disp, H, W]: zero-padded (2r+1)^2 window sums of the AD planes."""
         import torch
@@ -341,13 +363,16 @@ class BlockMatcher:
                                                   self._stream_ptr(stream)))
         return out_t
 
-    def set_stage_timing(self, on: bool) -> None:
-        """Record the host calls' upload / match / download split (default on; off saves the two
-        hipEvent markers between the stages, ~10 us per 1080p call, and stage_ms() then reads 0)."""
-        _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_STAGE_TIMING, 1.0 if on else 0.0))
+    def set_stage_timing(self, on) -> None:
+        """Record the host calls' upload / match / download split: True always, False never (stage_ms()
+        then reads 0), "auto" (the default) from the first stage_ms() call on.  Each recording costs two
+        hipEvent markers between the stages, ~10 us per 1080p call."""
+        v = 2.0 if on == "auto" else (1.0 if on else 0.0)
+        _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_STAGE_TIMING, v))
 
     def stage_ms(self) -> Tuple[float, float, float]:
-        """(upload, match, download) ms of the last host call (Device.cu:218,238/257,292)."""
+        """(upload, match, download) ms of the last host call (Device.cu:218,238/257,292).  With the
+        default "auto" timing the first read arms the recording for the calls after it."""
         u, m, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         _capi.check(self._lib.sm_last_stage_ms(self._h, ctypes.byref(u), ctypes.byref(m), ctypes.byref(d)))
         return u.value, m.value, d.value
@@ -552,16 +577,20 @@ def _default_matcher(W: int, H: int, D: int) -> BlockMatcher:
 def blockMatching_gpu(h_left, h_right, SADWindowSize: int, searchRange: int) -> np.ndarray:
     """Drop-in for ``blockMatching_gpu`` (Device.cu:173): returns the uint8 disparity map.
 
-    Prints the reference's stage lines ("upload data", "pre calculation"/"find corr",
-    "download data" in ms, Device.cu:218,238,257,292) only when ``SM_VERBOSE`` is set.
+    Prints the reference's four stage lines in ms, as Device.cu:218,238,257,292 always does:
+    "upload data", "pre calculation" (0: the AD cost is fused into the match), "find corr" and
+    "download data".  ``SM_QUIET`` in the environment silences them.
     """
+    import os
     L = _as_u8_image(h_left, "h_left")
     m = _default_matcher(L.shape[1], L.shape[0], searchRange)
+    quiet = bool(os.environ.get("SM_QUIET"))
+    if not quiet:
+        m.set_stage_timing(True)
     out = m.match(L, h_right, SADWindowSize, searchRange)
-    import os
-    if os.environ.get("SM_VERBOSE"):
+    if not quiet:
         u, c, d = m.stage_ms()
-        print(f"upload data : {u}\nfind corr : {c}\ndownload data : {d}")
+        print(f"upload data : {u:g}\npre calculation : 0\nfind corr : {c:g}\ndownload data : {d:g}")
     return out
 
 

@@ -36,6 +36,7 @@ EXPORTED = (
     "sm_match_device", "sm_slice_keys_device", "sm_keys_to_disp_device", "sm_stream_sync",
     "sm_bgr_to_gray_device", "sm_remap_u8_device", "sm_block_match_bgr_u8", "sm_median_u8_device",
     "sm_bgr_to_gray_u8", "sm_remap_u8", "sm_ad_volume_device", "sm_ad_volume_u8", "sm_sad_volume_device",
+    "sm_all_sad_device", "sm_all_sad_u8",
     "sm_stereo_rectify", "sm_init_rectify_map_device", "sm_init_rectify_map",
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
@@ -97,6 +98,8 @@ def load(path: str = LIB_PATH):
     L.sm_ad_volume_device.argtypes = [vp, vp, vp, i, i, i, i, vp, vp]
     L.sm_ad_volume_u8.argtypes = [vp, vp, vp, i, i, i, i, vp]
     L.sm_sad_volume_device.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp]
+    L.sm_all_sad_device.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp]
+    L.sm_all_sad_u8.argtypes = [vp, vp, vp, i, i, i, i, i, vp]
     L.sm_bgr_to_gray_device.argtypes = [vp, vp, i, i, i, i, vp, i, vp]
     L.sm_remap_u8_device.argtypes = [vp, vp, i, i, i, vp, vp, i, vp, i, vp]
     L.sm_block_match_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, i]

@@ -66,6 +66,11 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
 // staged box path (bm_staged.hip): u16 SAD volume from the AD volume, and WTA over the SAD volume
 // `ad` must have 8 readable bytes past its last plane (ensure_vol pads the handle's volume)
 hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, int D, uint16_t* sad, hipStream_t s);
+// getAllSAD's pixel-major uchar volume out[p * D + d] (255 where x + d > W): from the u16 SAD volume
+// (radius <= 7), or computed directly at any radius
+hipError_t launch_all_sad_transpose(const uint16_t* sad, int W, int H, int D, uint8_t* out, hipStream_t s);
+hipError_t launch_all_sad_generic(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int radius, int D,
+                                  uint8_t* out, hipStream_t s);
 // (`frames` consecutive frames of D planes each; frame f's map at disp + f * out_stride)
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,
                              int out_pitch, int64_t out_stride, hipStream_t s);

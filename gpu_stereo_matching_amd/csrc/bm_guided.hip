@@ -42,8 +42,10 @@
 #include "bm_common.h"
 #include "bm_guided.h"
 
-// The addtid stores set M0 inside their own asm statement and name it clobbered; these kernels have
-// no other M0 user (checked in the ISA), so clang's reserved-register warning is noise here.
+// Every addtid store sets M0 inside its own asm statement and names it clobbered (a
+// separate M0 write could be separated from its stores by a compiler-generated M0 use);
+// tools/check_lds_barriers.py --m0 checks the ISA for it.  Clang's reserved-register warning about
+// the clobber is noise here.
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace sm {
@@ -454,11 +456,6 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) rv[k] = STATS ? 0u : (uint32_t)rc[(a0 + k) * G::RBW];
         uint32_t T = 0u, Tp[2 * R + 1];
-        // M0 = this wave's first cs row for the add-TID stores below, set once per call.  An SALU write of
-        // M0 needs one wait state before an add-TID LDS instruction reads it (the compiler does not see
-        // the hazard inside the asm): s_nop 0.  Nothing else in this kernel uses M0 (checked in the
-        // ISA), and volatile asm statements keep their order, so every store below sees this value.
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(m0_cs) : "m0");
 #pragma unroll
         for (int k = 0; k < G::NV; ++k) {
             const uint32_t ad = __builtin_amdgcn_sad_u8(mul[k], rv[k], 0xFFFFFFF0u);
@@ -467,9 +464,12 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                 const uint32_t old = (k == 2 * R) ? 0u : Tp[(k - 2 * R - 1) % (2 * R + 1)];
                 const uint32_t val = m ? T - old : 0u;
                 // cs[(a0 + k - 2R) * CSS + lane]: lane-consecutive dwords, so ds_write_addtid_b32
-                // (2 LDS cycles per store instead of 4)
-                asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(val), "i"((k - 2 * R) * G::CSS * 4)
-                             : "memory");
+                // (2 LDS cycles per store instead of 4).  M0 (this wave's first cs row) is written in the
+                // same asm statement as the store that reads it, so no compiler-generated M0 use can
+                // fall between them; the SALU write needs one wait state before the add-TID LDS read
+                // of M0 (a hazard the compiler does not see inside asm): s_nop 0.
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tds_write_addtid_b32 %0 offset:%2"
+                             : : "v"(val), "s"(m0_cs), "i"((k - 2 * R) * G::CSS * 4) : "memory", "m0");
             }
             Tp[k % (2 * R + 1)] = T;
         }
@@ -559,8 +559,6 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         float2 v[NRW];
 #pragma unroll
         for (int k = 0; k < 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
-        // M0 = this wave's first mm row (plane A), set once per call as in S1V
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(m0_mm) : "m0");
 #pragma unroll
         for (int g = 0; g < G::RPS / 8; ++g) {
             if (g > 0) {
@@ -577,11 +575,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             for (int r = 8 * g; r < 8 * g + 8; ++r) {
                 sa += v[r + 2 * R].x;
                 sb += v[r + 2 * R].y;
-                // mmA / mmB [(RPS v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32
-                asm volatile("ds_write_addtid_b32 %0 offset:%2\n\tds_write_addtid_b32 %1 offset:%3"
+                // mmA / mmB [(RPS v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32, with
+                // M0 (this wave's first mm row, plane A) set inside the same asm statement as in S1V
+                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                             "ds_write_addtid_b32 %0 offset:%3\n\tds_write_addtid_b32 %1 offset:%4"
                              :
-                             : "v"(sa), "v"(sb), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
-                             : "memory");
+                             : "v"(sa), "v"(sb), "s"(m0_mm), "i"(r * G::MSA * 4), "i"(r * G::MSA * 4 + G::MM_PLANE)
+                             : "memory", "m0");
                 sa -= v[r].x;
                 sb -= v[r].y;
             }

@@ -301,6 +301,72 @@ __global__ __launch_bounds__(kST) void volume_wta_kernel(const uint16_t* __restr
     }
 }
 
+// getAllSAD (BlockMatching.cpp:191-261): the SAD volume pixel-major, data_dm[p * D + d], each sum stored
+// as uchar (truncated mod 256, :258) and 255 where x + d > W (:245-249).  The d-major u16 volume of
+// box_sad_kernel is transposed through LDS, 64 pixels per block: the loads read 128 B of one plane per
+// wave and d, and the block's 64 * D output bytes are one contiguous run written as dwords.  The low 8
+// bits of a u16 sum are the low 8 bits of the true sum, so uchar truncation of either is the same.
+constexpr int kAsPx = 64;
+__global__ __launch_bounds__(kST) void all_sad_transpose_kernel(const uint16_t* __restrict__ sad, int W, int64_t P,
+                                                                int D, int Dp, uint8_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];   // [kAsPx][Dp]
+    const int64_t p0 = (int64_t)blockIdx.x * kAsPx;
+    const int npx = P - p0 < kAsPx ? (int)(P - p0) : kAsPx;
+    // a thread always handles pixel px = tid mod 64 (its e advances by 256 = 4 * 64): one x per thread
+    const int px = threadIdx.x & (kAsPx - 1);
+    const int x = (int)((p0 + px) % W);
+    if (px < npx) {
+        for (int d = threadIdx.x >> 6; d < D; d += kST / kAsPx) {
+            const uint16_t v = sad[(int64_t)d * P + p0 + px];
+            tile[px * Dp + d] = x + d > W ? (uint8_t)255 : (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    uint8_t* o = out + p0 * D;
+    const int n = npx * D;
+    if ((D & 3) == 0 && (reinterpret_cast<uintptr_t>(o) & 3) == 0) {
+        for (int e = 4 * threadIdx.x; e < n; e += 4 * kST) {
+            const int q = e / D, d = e - q * D;
+            *reinterpret_cast<uint32_t*>(o + e) = *reinterpret_cast<const uint32_t*>(tile + q * Dp + d);
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += kST) {
+            const int q = e / D;
+            o[e] = tile[q * Dp + (e - q * D)];
+        }
+    }
+}
+
+// getAllSAD at any radius (the u16 volume's box_sad_kernel covers r <= 7): one thread per (row, d),
+// lanes over d, walking the row with a running sum of column sums; each column sum is its (clipped)
+// 2r + 1 taps of |L - R(x - d)|, zero where x < d (Device.cu:27-31).  The stores of one wave and column
+// are 64 consecutive bytes of the pixel-major volume.  Not a performance path: the reference's
+// getAllSAD is a CPU debugging aid (BlockMatching.h:11, Device.cu:265-268).
+__global__ __launch_bounds__(kST) void all_sad_generic_kernel(const uint8_t* __restrict__ L,
+                                                              const uint8_t* __restrict__ R, int W, int H, int pitch,
+                                                              int radius, int D, uint8_t* __restrict__ out) {
+    const int d = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * (kST / 64) + (threadIdx.x >> 6);
+    if (d >= D || y >= H) return;
+    const int y0 = max(0, y - radius), y1 = min(H - 1, y + radius);
+    auto colsum = [&](int xc) -> uint32_t {
+        if (xc < 0 || xc >= W || xc < d) return 0u;
+        uint32_t s = 0;
+        for (int yy = y0; yy <= y1; ++yy) {
+            const int a = L[(int64_t)yy * pitch + xc], b = R[(int64_t)yy * pitch + xc - d];
+            s += (uint32_t)(a > b ? a - b : b - a);
+        }
+        return s;
+    };
+    uint32_t S = 0;
+    for (int j = -radius; j <= radius; ++j) S += colsum(j);
+    uint8_t* o = out + (int64_t)y * W * D + d;
+    for (int x = 0; x < W; ++x) {
+        o[(int64_t)x * D] = x + d > W ? (uint8_t)255 : (uint8_t)S;
+        S += colsum(x + radius + 1) - colsum(x - radius);
+    }
+}
+
 template <int R>
 hipError_t launch_box_sad_r(const uint8_t* ad, int W, int H, int D, uint16_t* sad, hipStream_t s) {
     const int strips = (W + kSO - 1) / kSO;
@@ -333,6 +399,24 @@ hipError_t launch_box_sad_volume(const uint8_t* ad, int W, int H, int radius, in
         default: return hipErrorInvalidValue;
     }
 #undef SM_BOX_SAD_CASE
+}
+
+hipError_t launch_all_sad_transpose(const uint16_t* sad, int W, int H, int D, uint8_t* out, hipStream_t s) {
+    const int64_t P = (int64_t)W * H;
+    const int64_t blocks = (P + kAsPx - 1) / kAsPx;
+    if (W <= 0 || H <= 0 || D < 1 || D > kMaxDisp || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const int Dp = ((D + 3) & ~3) + 4;   // dword-aligned tile rows, offset by one bank per pixel
+    hipLaunchKernelGGL(all_sad_transpose_kernel, dim3((unsigned)blocks), dim3(kST), (size_t)(kAsPx * Dp), s, sad, W, P,
+                       D, Dp, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_all_sad_generic(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int radius, int D,
+                                  uint8_t* out, hipStream_t s) {
+    if (W <= 0 || H <= 0 || D < 1 || D > kMaxDisp || radius < 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(all_sad_generic_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)((H + 3) / 4)), dim3(kST), 0,
+                       s, L, R, W, H, pitch, radius, D, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,

@@ -59,7 +59,10 @@ struct sm_handle {
     size_t bgr_bytes = 0;
     float guided_eps = 6.5025f;  // 1e-4 * 255^2 (AD units)
     int staged_group = 8;        // SM_STAGED frames per launch group (SM_PARAM_STAGED_GROUP)
-    bool stage_timing = true;    // host calls record the upload / match / download split (SM_PARAM_STAGE_TIMING)
+    // host calls record the upload / match / download split (SM_PARAM_STAGE_TIMING): 0 off, 1 on, 2 auto
+    // (default: on once sm_last_stage_ms has been called on the handle, or when SM_VERBOSE is set)
+    int stage_timing = 2;
+    bool stage_requested = false;
     // The workspaces above are shared by every call on the handle while calls run on the stream
     // they are given: the end of each pass is recorded here, and a pass on another stream waits
     // for it first, so two streams never write the same workspace at once.
@@ -386,6 +389,11 @@ uint8_t* host_block_device_ptr(void* p, size_t bytes) {
     return static_cast<uint8_t*>(dbase) + ((uintptr_t)p - base);
 }
 
+bool verbose_env() {
+    static const bool on = getenv("SM_VERBOSE") != nullptr;
+    return on;
+}
+
 // SM_ZERO_COPY=0 keeps the device buffer + download for every call (A/B timing)
 bool zero_copy_enabled() {
     static const bool on = [] {
@@ -462,7 +470,7 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
     }
     // stage split events (SM_PARAM_STAGE_TIMING): each costs a marker between the copy and compute
     // queues, ~10 us per 1080p call for the two (profiles/microbench/r03_roundtrip_pair_block.txt)
-    const bool ev = h->stage_timing;
+    const bool ev = h->stage_timing == 1 || (h->stage_timing == 2 && (h->stage_requested || verbose_env()));
     if (ev) SM_HIP(hipEventRecord(h->ev[1], s));
     rc = run_device(h, h->d_left, dR, width, height, width, 1, P, radius, num_disp, flags,
                     mapped ? mapped : h->d_disp, mapped ? out_pitch : width, P, right_out ? aux : nullptr,
@@ -758,14 +766,15 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
     const int64_t P = (int64_t)W * H;
     const DslicePlan p = dslice_plan(P, D, n, k);
     const DsliceWs w = dslice_ws(h, p);
-    SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    // every failure of phase 2 goes through bail, so the others stop polling for this member
     auto bail = [&](int code, const char* what) {
         sync->abort.store(true);
-        (void)api->abort(*comm);
+        if (*comm) (void)api->abort(*comm);
         *comm = nullptr;
         return fail(code, "d-slice member %d: %s", k, what);
     };
+    if (hipSetDevice(h->device) != hipSuccess) return bail(SM_ERR_LAUNCH, "hipSetDevice failed");
     if (dslice_fault(k, "collective")) return bail(SM_ERR_LAUNCH, "injected fault (collective)");
     // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
     if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, guided ? ncclInt32 : ncclUint32, ncclMin, *comm, s) !=
@@ -785,8 +794,8 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
         std::this_thread::yield();
     }
     if (k == 0) {
-        SM_HIP(copy2d(disp_out, out_pitch, w.map, W, W, H, hipMemcpyDeviceToHost, s));
-        SM_HIP(hipStreamSynchronize(s));
+        const hipError_t e = copy2d(disp_out, out_pitch, w.map, W, W, H, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return bail(SM_ERR_LAUNCH, "map download failed");
     }
     return SM_OK;
 }
@@ -869,10 +878,13 @@ SM_API int sm_create(int device, int max_width, int max_height, int max_disp, sm
     h->max_d = max_disp;
     const size_t P = (size_t)max_width * max_height;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    // the pair's device frames are one allocation (d_right = d_left + P), so a host pair that sits in one
-    // block (right frame right after the left one) uploads as one DMA copy
-    if (e == hipSuccess) e = hipMalloc(&h->d_left, 2 * P);
-    if (e == hipSuccess) h->d_right = h->d_left + P;
+    // the pair's device frames are one allocation, so a host pair that sits in one block (right frame
+    // right after the left one) uploads as one DMA copy into d_left .. d_left + 2P (host_match_rows then
+    // reads the right frame at d_left + P).  d_right itself starts 256-B aligned (at
+    // d_left + P it was not even dword-aligned for odd max sizes).
+    const size_t Pa = (P + 255) & ~(size_t)255;
+    if (e == hipSuccess) e = hipMalloc(&h->d_left, 2 * Pa);
+    if (e == hipSuccess) h->d_right = h->d_left + Pa;
     if (e == hipSuccess) e = hipMalloc(&h->d_disp, P);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming);
@@ -920,12 +932,22 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
         const int g = (int)value;
         if ((float)g != value || g < 1 || g > kStagedGroup)
             return fail(SM_ERR_INVALID_ARG, "staged launch group must be an integer in [1, %d]", kStagedGroup);
+        if (g < h->staged_group && h->d_vol) {
+            // a smaller group bounds the workspace from now on: drop the larger volume once
+            // the handle's pending work is done, and let the next staged call allocate the new size
+            SM_HIP(hipSetDevice(h->device));
+            SM_HIP(hipStreamSynchronize(h->stream));
+            if (h->scratch_pending) SM_HIP(hipEventSynchronize(h->scratch_ev));
+            SM_HIP(hipFree(h->d_vol));
+            h->d_vol = nullptr;
+            h->vol_bytes = 0;
+        }
         h->staged_group = g;
         return SM_OK;
     }
     if (param == SM_PARAM_STAGE_TIMING) {
-        if (value != 0.f && value != 1.f) return fail(SM_ERR_INVALID_ARG, "stage timing is 0 or 1");
-        h->stage_timing = value != 0.f;
+        if (value != 0.f && value != 1.f && value != 2.f) return fail(SM_ERR_INVALID_ARG, "stage timing is 0, 1 or 2");
+        h->stage_timing = (int)value;
         return SM_OK;
     }
 
@@ -980,6 +1002,7 @@ SM_API int sm_last_staged_kernel_ms(sm_handle* h, float* ad_ms, float* sad_ms, f
 
 SM_API int sm_last_stage_ms(sm_handle* h, float* upload_ms, float* match_ms, float* download_ms) {
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    h->stage_requested = true;   // auto mode: the calls from now on record the split
     if (upload_ms) *upload_ms = h->stage_ms[0];
     if (match_ms) *match_ms = h->stage_ms[1];
     if (download_ms) *download_ms = h->stage_ms[2];
@@ -1262,6 +1285,74 @@ SM_API int sm_sad_volume_device(sm_handle* h, const uint8_t* d_left, const uint8
     SM_HIP(sm::launch_ad_volume(d_left, d_right, width, height, pitch, (int64_t)pitch * height, 1, num_disp,
                                 h->d_vol, P * num_disp, s));
     SM_HIP(sm::launch_box_sad_volume(h->d_vol, width, height, radius, num_disp, d_sad, s));
+    return SM_OK;
+}
+
+namespace {
+// getAllSAD's volume (P * D device bytes, pixel-major) on stream s into `out`, or, with out == nullptr,
+// into the first P * D bytes of the handle's d_vol (*where says which).  r <= 7 and W <= 4096: AD volume
+// -> u16 SAD volume in d_vol -> transpose (the AD volume at the start of d_vol is consumed by the SAD
+// kernel before the transpose overwrites it, in stream order); otherwise the direct kernel.
+int run_all_sad(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int radius, int D,
+                uint8_t* out, uint8_t** where, hipStream_t s) {
+    const int64_t P = (int64_t)W * H;
+    if (radius <= sm::kMaxFastRadius && W <= 4096) {
+        const int64_t ad_bytes = (P * D + 255) & ~(int64_t)255;   // the u16 volume starts 256-B aligned
+        int rc = ensure_vol(h, (size_t)(ad_bytes + 2 * P * D));
+        if (rc) return rc;
+        uint16_t* sad = reinterpret_cast<uint16_t*>(h->d_vol + ad_bytes);
+        if (!out) out = h->d_vol;
+        SM_HIP(sm::launch_ad_volume(L, R, W, H, pitch, (int64_t)pitch * H, 1, D, h->d_vol, P * D, s));
+        SM_HIP(sm::launch_box_sad_volume(h->d_vol, W, H, radius, D, sad, s));
+        SM_HIP(sm::launch_all_sad_transpose(sad, W, H, D, out, s));
+    } else {
+        if (!out) {
+            int rc = ensure_vol(h, (size_t)(P * D));
+            if (rc) return rc;
+            out = h->d_vol;
+        }
+        SM_HIP(sm::launch_all_sad_generic(L, R, W, H, pitch, radius, D, out, s));
+    }
+    if (where) *where = out;
+    return SM_OK;
+}
+}  // namespace
+
+SM_API int sm_all_sad_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                             int pitch, int radius, int num_disp, uint8_t* d_out, void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!d_left || !d_right || !d_out) return fail(SM_ERR_INVALID_ARG, "null device pointer");
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    // d_vol is handle workspace: order after a pass of this handle on another stream, as run_device does
+    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    rc = run_all_sad(h, d_left, d_right, width, height, pitch, radius, num_disp, d_out, nullptr, s);
+    SM_HIP(hipEventRecord(h->scratch_ev, s));
+    h->scratch_stream = s;
+    h->scratch_pending = true;
+    return rc;
+}
+
+SM_API int sm_all_sad_u8(sm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height, int pitch,
+                         int radius, int num_disp, uint8_t* sad_out) {
+    int rc = check_geometry(h, width, height, pitch, radius, num_disp);
+    if (rc) return rc;
+    if (!left || !right || !sad_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    const size_t need = (size_t)width * height * num_disp;
+    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    uint8_t* vol = nullptr;
+    rc = run_all_sad(h, h->d_left, h->d_right, width, height, width, radius, num_disp, nullptr, &vol, s);
+    if (rc) return rc;
+    SM_HIP(hipMemcpyAsync(sad_out, vol, need, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    h->scratch_pending = false;   // the handle's stream has drained
     return SM_OK;
 }
 

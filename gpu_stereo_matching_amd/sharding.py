@@ -29,14 +29,28 @@ def frame_shard(n_frames: int, rank: int, world: int) -> List[int]:
     return list(range(lo, hi))
 
 
+def dslice_plan_py(pixels: int, num_disp: int, rank: int, world: int) -> Tuple[int, int, int, int]:
+    """The same plan as sm_dslice_plan in pure Python (host arithmetic, no device): used where the
+    HIP library is not built (CPU-only gloo ranks); tests/test_dslice_plan.py checks that both agree
+    whenever the library is present."""
+    if pixels <= 0 or num_disp < 1 or world < 1 or not 0 <= rank < world:
+        raise ValueError(f"d-slice plan: pixels {pixels}, num_disp {num_disp}, member {rank} of {world}")
+    chunk = (pixels + world - 1) // world
+    return rank * num_disp // world, (rank + 1) * num_disp // world, chunk, chunk * world
+
+
 def dslice_plan(pixels: int, num_disp: int, rank: int, world: int) -> Tuple[int, int, int, int]:
     """(d_lo, d_hi, chunk, padded_pixels) of `rank`: the library's own plan (sm_dslice_plan), the
     one sm_group_dslice_block_match_u8 uses, so the torch and C paths cannot drift apart.  Rank k
     scans d in [k*D/G, (k+1)*D/G) (empty when G > D); the keys are padded to G*chunk pixels and the
-    reduce-scatter hands rank k pixels [k*chunk, (k+1)*chunk)."""
+    reduce-scatter hands rank k pixels [k*chunk, (k+1)*chunk).  Without the HIP library (a CPU-only
+    process) the pure-Python twin dslice_plan_py gives the same numbers."""
     import ctypes
     from . import _capi
-    lib = _capi.load()
+    try:
+        lib = _capi.load()
+    except ImportError:
+        return dslice_plan_py(pixels, num_disp, rank, world)
     lo, hi = ctypes.c_int(), ctypes.c_int()
     chunk, padded = ctypes.c_int64(), ctypes.c_int64()
     _capi.check(lib.sm_dslice_plan(pixels, num_disp, world, rank, ctypes.byref(lo), ctypes.byref(hi),

@@ -56,8 +56,10 @@ enum {
                                SM_AGG_GUIDED or SM_LR_CHECK, radius <= 7.  Frames run in launch
                                groups of up to 8 (SM_PARAM_STAGED_GROUP), and the handle keeps the
                                volumes' workspace, 3*P*D (+ P with SM_MEDIAN) bytes per frame of a
-                               group, for its lifetime: ~6.4 GB at 1080p D=128 with 8-frame groups
-                               (capped at 8 GiB), ~0.8 GB with groups of 1 */
+                               group: ~6.4 GB at 1080p D=128 with 8-frame groups (capped at 8 GiB),
+                               ~0.8 GB with groups of 1.  Lowering SM_PARAM_STAGED_GROUP frees the
+                               workspace (after the handle's pending work), so the next staged call
+                               allocates the smaller size */
 };
 
 /* ---- scalar parameters (sm_set_param_f) ---- */
@@ -65,9 +67,12 @@ enum {
     SM_PARAM_GUIDED_EPS = 1,  /* guided-filter epsilon in AD^2 units (default 6.5025 = 1e-4 * 255^2) */
     SM_PARAM_STAGED_GROUP = 2, /* SM_STAGED frames per launch group, 1..8 (default 8): bounds the
                                   handle's staged workspace (see SM_STAGED) */
-    SM_PARAM_STAGE_TIMING = 3  /* 1 (default): host calls record the upload / match / download split
-                                  read by sm_last_stage_ms; 0: they skip those hipEvents (~10 us less
-                                  per 1080p call) and sm_last_stage_ms reports 0 */
+    SM_PARAM_STAGE_TIMING = 3  /* whether host calls record the upload / match / download split read by
+                                  sm_last_stage_ms with two hipEvents (each a marker between the copy and
+                                  compute queues, ~10 us per 1080p call together).  2 (default, auto):
+                                  recorded once sm_last_stage_ms has been called on the handle (the calls
+                                  after that first read), or in every call when the environment sets
+                                  SM_VERBOSE; 1: always; 0: never, and sm_last_stage_ms reports 0 */
 };
 
 typedef struct sm_handle sm_handle;
@@ -108,7 +113,9 @@ SM_API int sm_block_match_lr_u8(sm_handle *h, const uint8_t *left, const uint8_t
 
 /* Per-stage timings of the last sm_block_match_* call in ms (hipEvents), mirroring the
  * reference's "upload data / pre calculation / find corr / download data" printouts
- * (Device.cu:218,238,257,292).  Any pointer may be NULL. */
+ * (Device.cu:218,238,257,292; "pre calculation" is fused into the match stage here).  With the
+ * default SM_PARAM_STAGE_TIMING (auto) the first call of this function turns the recording on for
+ * the handle's later calls; a call made while recording was off reads 0.  Any pointer may be NULL. */
 SM_API int sm_last_stage_ms(sm_handle *h, float *upload_ms, float *match_ms, float *download_ms);
 
 /* Kernel times (ms, hipEvents on the launch stream) of the last SM_STAGED pass, per frame: the
@@ -188,6 +195,17 @@ SM_API int sm_ad_volume_u8(sm_handle *h, const uint8_t *left, const uint8_t *rig
  * without their uint8 truncation).  d_sad holds num_disp*width*height uint16. */
 SM_API int sm_sad_volume_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
                                 int pitch, int radius, int num_disp, uint16_t *d_sad, void *stream);
+
+/* getAllSAD (BlockMatching.cpp:191-261; BlockMatching.h:11): every window SAD, PIXEL-major
+ * sad[(y*width + x)*num_disp + d], stored as uint8 (the reference's uchar store truncates mod 256,
+ * :258), and 255 where x + d > width (:245-249).  Any radius (r <= 7 and width <= 4096 go through the
+ * AD and u16 SAD volumes of SM_STAGED plus a transpose; other sizes through a direct kernel).
+ * Device form: d_sad holds width*height*num_disp bytes, asynchronous on `stream`, uses the handle's
+ * volume workspace (~4*P*num_disp bytes).  Host form: synchronous, sad_out likewise sized. */
+SM_API int sm_all_sad_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
+                             int pitch, int radius, int num_disp, uint8_t *d_sad, void *stream);
+SM_API int sm_all_sad_u8(sm_handle *h, const uint8_t *left, const uint8_t *right, int width, int height,
+                         int pitch, int radius, int num_disp, uint8_t *sad_out);
 
 /* ---- post-filter ----
  * (2r+1)^2 median with replicate borders, r in 1..3: ctmf (STMatching/ctmf.c:378-433) as called

@@ -4,7 +4,8 @@
 //   void remap_gpu(Mat &left, Mat &right, Mat &mapX1, Mat &mapY1, Mat &mapX2, Mat &mapY2,
 //                  int rows, int cols, int total, uchar *result);
 //   void cvtColor_gpu(uchar3 *src, uchar *dst, int rows, int cols);
-// and BlockMatching.h's testBM / getDisp / PreCal (BlockMatching.h:8-10), on top of the C ABI in
+// and all of BlockMatching.h (BlockMatching.h:8-15: testBM / PreCal / getDisp / getAllSAD and the
+// compareDiff / compareDisp / compareSAD checks), on top of the C ABI in
 // sm_hip.h, so a Main.cpp / Caller.cpp (singleFrame, remapTest, cvtColorTest) shaped caller
 // compiles and runs unchanged apart from the include.  Host-only:
 // compile it with a plain C++ compiler (it declares the host type uchar3 the reference's callers
@@ -16,13 +17,19 @@
 // member, or sm::Mat's (rows, cols, CV_8UC1) constructor, is accepted.
 //
 // Behaviour vs the reference (Device.cu:173-301):
-//   same arguments, same disparity values (bit-exact), same stdout stage lines
-//   ("upload data : ms", "find corr : ms", "download data : ms") when SM_VERBOSE is set;
+//   same arguments, same disparity values (bit-exact), same four stdout stage lines in ms
+//   ("upload data", "pre calculation", "find corr", "download data", Device.cu:218,238,257,292;
+//   "pre calculation" reads 0 because the AD cost is fused into the match kernel, and a multi-GPU
+//   group call, which has no single upload/download, reports its whole wall time as "find corr");
+//   BlockMatching.h's functions print BlockMatching.cpp's lines ("prep location", "precalculate
+//   diff", "main loop", in seconds) with the GPU call's wall time on the last line the reference
+//   prints for that function; SM_QUIET silences every line;
 //   the output Mat owns its memory (the reference wraps a leaked new[] buffer, :185/:300);
 //   errors are reported on std::cerr and leave an all-zero map, like the reference's silent
 //   launch failure but visible.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -95,6 +102,10 @@ struct Size {                            // cv::Size: (width, height)
 
 namespace detail {
 
+// SM_QUIET in the environment silences the reference's stdout lines (stage timings, BlockMatching.cpp's
+// step lines)
+inline bool quiet() { return std::getenv("SM_QUIET") != nullptr; }
+
 // SM_DEVICE=k picks the device; SM_DEVICES=a,b,... (two or more) also builds a group handle
 // (sm_create_group) over those devices, and blockMatching_gpu / testBM / getDisp then split each
 // frame into row bands, one per device (bit-identical results).  SM_GROUP_MODE=dslice splits the
@@ -135,6 +146,8 @@ struct Engine {
             h = nullptr;
             return false;
         }
+        // the stage lines read the upload / match / download split of every call
+        if (!quiet()) sm_set_param_f(h, SM_PARAM_STAGE_TIMING, 1.f);
         // the d-slice mode runs through a group even on one device (a one-rank communicator)
         const char* mode = std::getenv("SM_GROUP_MODE");
         std::vector<int> gdevs = devs;
@@ -161,9 +174,11 @@ template <typename M> inline void make_output(M& out, int rows, int cols) { out.
 }  // namespace detail
 
 // Mat-agnostic implementation (cv::Mat or sm::Mat).
+// stage_lines: print Device.cu's four stage lines (blockMatching_gpu); BlockMatching.h's functions
+// print their own.
 template <typename M>
 inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int SADWindowSize, int searchRange,
-                          unsigned flags = SM_AGG_BOX) {
+                          unsigned flags = SM_AGG_BOX, bool stage_lines = false) {
     const int rows = h_left.rows, cols = h_left.cols;
     detail::make_output(h_disparity, rows, cols);
     if (h_right.rows != rows || h_right.cols != cols) {
@@ -174,6 +189,7 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     if (!e.ensure(cols, rows, searchRange)) return SM_ERR_DEVICE;
     const char* mode = std::getenv("SM_GROUP_MODE");
     const bool dslice = e.g && mode && std::string(mode) == "dslice" && (flags & ~(unsigned)SM_AGG_GUIDED) == 0u;
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = dslice ? sm_group_dslice_block_match_u8(e.g, h_left.data, h_right.data, cols, rows,
                                                      (int)detail::row_step(h_left), SADWindowSize, searchRange, flags,
                                                      h_disparity.data, (int)detail::row_step(h_disparity))
@@ -188,11 +204,15 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
         for (int r = 0; r < rows; ++r) std::memset(h_disparity.data + (size_t)r * detail::row_step(h_disparity), 0, cols);
         return rc;
     }
-    if (std::getenv("SM_VERBOSE") && !e.g) {
+    if (stage_lines && !detail::quiet()) {
         float up = 0, mt = 0, dn = 0;
-        sm_last_stage_ms(e.h, &up, &mt, &dn);
+        if (e.g)   // row bands / d-slices on several devices: one wall time, no single copy stage
+            mt = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        else
+            sm_last_stage_ms(e.h, &up, &mt, &dn);
         std::cout << "upload data : " << up << std::endl;        // Device.cu:218
-        std::cout << "find corr : " << mt << std::endl;          // Device.cu:257 (pre calculation fused)
+        std::cout << "pre calculation : " << 0 << std::endl;     // Device.cu:238 (fused into find corr)
+        std::cout << "find corr : " << mt << std::endl;          // Device.cu:257
         std::cout << "download data : " << dn << std::endl;      // Device.cu:292
     }
     return rc;
@@ -239,37 +259,101 @@ using SmHostMat = sm::Mat;
 #endif
 inline void blockMatching_gpu(SmHostMat& h_left, SmHostMat& h_right, SmHostMat& h_disparity, int SADWindowSize,
                               int searchRange) {
-    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange);
+    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange, SM_AGG_BOX, true);
 }
 inline void remap_gpu(SmHostMat& left, SmHostMat& right, SmHostMat& mapX1, SmHostMat& mapY1, SmHostMat& mapX2,
                       SmHostMat& mapY2, int rows, int cols, int /*total*/, uchar* result) {
     sm::remap(left, right, mapX1, mapY1, mapX2, mapY2, rows, cols, result);
 }
 
-// ---- BlockMatching.h (BlockMatching.h:8-10): the reference's CPU entry points, same signatures
+// ---- BlockMatching.h (BlockMatching.h:8-15): the reference's CPU entry points, same signatures
 //      and outputs, computed on the GPU ----
+namespace sm {
+namespace detail {
+// BlockMatching.cpp's step lines (cout << label << seconds, :32,49,84 / :136,153,188 / :215,232).  The
+// tap table and the AD volume are not separate steps here (0); `main` is the GPU call's wall time.
+inline void cpu_lines(double main_s, bool with_main) {
+    if (quiet()) return;
+    std::cout << "prep location " << 0 << std::endl;
+    std::cout << "precalculate diff " << (with_main ? 0.0 : main_s) << std::endl;
+    if (with_main) std::cout << "main loop " << main_s << std::endl;
+}
+inline double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace detail
+}  // namespace sm
+
 // testBM / getDisp: the disparity map of getDisp (BlockMatching.cpp:7-87, :111-189), bit-exact.
 inline void testBM(const SmHostMat& left0, const SmHostMat& right0, SmHostMat& disparity, int SAD, int searchRange) {
+    const auto t0 = std::chrono::steady_clock::now();
     sm::block_matching(left0, right0, disparity, SAD, searchRange);
+    sm::detail::cpu_lines(sm::detail::seconds_since(t0), true);
 }
 inline void getDisp(const SmHostMat& left0, const SmHostMat& right0, uchar* disparity, int SAD, int searchRange) {
     sm::detail::Engine& e = sm::detail::engine();
     if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
     const int lp = (int)sm::detail::row_step(left0);
+    const auto t0 = std::chrono::steady_clock::now();
     if ((e.g ? sm_group_block_match_u8(e.g, left0.data, right0.data, left0.cols, left0.rows, lp, SAD, searchRange,
                                        SM_AGG_BOX, disparity, left0.cols)
              : sm_block_match_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, lp, SAD, searchRange,
                                  SM_AGG_BOX, disparity, left0.cols)) != SM_OK)
         std::cerr << "getDisp: " << sm_last_error_string() << std::endl;
+    sm::detail::cpu_lines(sm::detail::seconds_since(t0), true);
 }
 // PreCal (BlockMatching.cpp:89-109): the AD volume, searchRange d-major planes of rows*cols bytes.
-// Entries with x < d are written as 0 (the reference leaves them at the caller's memset 0).
+// Entries with x < d are written as 0 (the reference leaves them at the caller's memset 0).  The
+// reference's PreCal prints nothing.
 inline void PreCal(const SmHostMat& left0, const SmHostMat& right0, uchar* dif_, int /*SAD*/, int searchRange) {
     sm::detail::Engine& e = sm::detail::engine();
     if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
     if (sm_ad_volume_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, (int)sm::detail::row_step(left0),
                         searchRange, dif_) != SM_OK)
         std::cerr << "PreCal: " << sm_last_error_string() << std::endl;
+}
+// getAllSAD (BlockMatching.cpp:191-261): every window SAD, pixel-major data_dm[p * searchRange + d],
+// truncated to uchar, 255 where col + d > cols; bit-exact (sm_all_sad_u8).
+inline void getAllSAD(const SmHostMat& left0, const SmHostMat& right0, uchar* data_dm, int SAD, int searchRange) {
+    sm::detail::Engine& e = sm::detail::engine();
+    if (!e.ensure(left0.cols, left0.rows, searchRange)) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (sm_all_sad_u8(e.h, left0.data, right0.data, left0.cols, left0.rows, (int)sm::detail::row_step(left0), SAD,
+                      searchRange, data_dm) != SM_OK)
+        std::cerr << "getAllSAD: " << sm_last_error_string() << std::endl;
+    sm::detail::cpu_lines(sm::detail::seconds_since(t0), false);
+}
+// The reference's debugging cross-checks (BlockMatching.cpp:263-308), same output format: the
+// reference result is recomputed (PreCal / getDisp / getAllSAD above) and every mismatching index is
+// printed; compareDiff and compareSAD end with "-1" and no newline.
+inline void compareDiff(const SmHostMat& left0, const SmHostMat& right0, uchar* GPUresult, int SADWindowSize,
+                        int searchRange, int total) {
+    std::vector<uchar> ref((size_t)total * searchRange, 0);
+    PreCal(left0, right0, ref.data(), SADWindowSize, searchRange);
+    for (size_t i = 0; i < (size_t)searchRange * total; i++)
+        if (ref[i] != GPUresult[i]) std::cout << i << std::endl;
+    std::cout << -1;
+}
+inline void compareDisp(const SmHostMat& left, const SmHostMat& right, uchar* GPUresult, int SADWindowSize,
+                        int searchRange, int cols, int rows) {
+    std::vector<uchar> ref((size_t)rows * cols);
+    getDisp(left, right, ref.data(), SADWindowSize, searchRange);
+    for (size_t i = 0; i < (size_t)rows; i++)
+        for (size_t j = 0; j < (size_t)cols; j++)
+            if (ref[i * cols + j] != GPUresult[i * cols + j]) {
+                std::cout << "[" << i << ":" << j << "]" << std::endl;
+                std::cout << "CPU = " << (int)ref[i * cols + j] << ", GPU = " << (int)GPUresult[i * cols + j]
+                          << std::endl;
+            }
+}
+inline void compareSAD(const SmHostMat& left, const SmHostMat& right, uchar* GPUresult, int SADWindowSize,
+                       int searchRange, int cols, int rows) {
+    const size_t total = (size_t)rows * cols;
+    std::vector<uchar> allSAD((size_t)searchRange * total, 255);
+    getAllSAD(left, right, allSAD.data(), SADWindowSize, searchRange);
+    for (size_t i = 0; i < (size_t)searchRange * total; i++)
+        if (allSAD[i] != GPUresult[i]) std::cout << i << std::endl;
+    std::cout << -1;
 }
 
 // ---- Utility.h (Utility.h:26-27, :42): the calibration load and Rectify in front of remap_gpu ----

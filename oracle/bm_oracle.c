@@ -211,6 +211,60 @@ ORA_API int ora_get_disp(const uint8_t *L, const uint8_t *R, int W, int H, int r
 }
 
 /* ------------------------------------------------------------------------- */
+/* a6: literal restatement of getAllSAD (BlockMatching.cpp:191-261), the CPU  */
+/* twin of the dead kernalFindAllSAD (Device.cu:67-103): every window SAD,    */
+/* pixel-major out[p*D + d], stored into uchar (truncated mod 256, :258), and */
+/* 255 where col + d > W (:245-249).  No early exit in this loop nest.  The   */
+/* memset of the first P bytes (:201) is overwritten by the loop, which       */
+/* writes every one of the P*D entries.                                        */
+/*   dif: caller-provided scratch of P*D bytes, or NULL to allocate.          */
+/* ------------------------------------------------------------------------- */
+ORA_API int ora_get_all_sad(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                            uint8_t *out, uint8_t *dif)
+{
+    const int64_t P = (int64_t)W * H;
+    const int win = 2 * radius + 1;
+    const int taps = win * win;
+    uint8_t *own = NULL;
+    if (!dif) {
+        own = (uint8_t *)malloc((size_t)(P * D));
+        if (!own) return -1;
+        dif = own;
+    }
+    int *tdx = (int *)malloc(sizeof(int) * taps);
+    int *tdy = (int *)malloc(sizeof(int) * taps);
+    int64_t *toff = (int64_t *)malloc(sizeof(int64_t) * taps);
+    for (int t = 0; t < taps; ++t) {                        /* :209-212 */
+        tdx[t] = t % win - radius;
+        tdy[t] = t / win - radius;
+        toff[t] = tdx[t] + (int64_t)tdy[t] * W;
+    }
+    ora_precal(L, R, W, H, D, dif);                         /* :221-230 */
+    memset(out, 0, (size_t)P);                              /* :201 */
+    for (int64_t p = 0; p < P; ++p) {
+        const int col = (int)(p % W), row = (int)(p / W);
+        for (int d = 0; d < D; ++d) {
+            if (col + d > W) {                              /* :245-249 */
+                out[p * D + d] = 255;
+                continue;
+            }
+            const uint8_t *plane = dif + (int64_t)d * P;
+            int acc = 0;
+            for (int t = 0; t < taps; ++t) {
+                int c = col + tdx[t];
+                if (c >= W || c < 0) continue;              /* :253 */
+                int rr = row + tdy[t];
+                if (rr >= H || rr < 0) continue;            /* :255 */
+                acc += plane[p + toff[t]];
+            }
+            out[p * D + d] = (uint8_t)acc;                  /* :258, uchar store */
+        }
+    }
+    free(tdx); free(tdy); free(toff); free(own);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* a3: independent restatement of the same map as                            */
 /*   zero-padded (2r+1)^2 box sum of each AD plane                           */
 /*   + validity d <= W - x (the break at BlockMatching.cpp:166/Device.cu:44) */

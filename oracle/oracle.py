@@ -42,6 +42,7 @@ def lib():
         L.ora_bgr_to_gray.argtypes = [_u8p, ctypes.c_int64, ctypes.c_int, _u8p]
         L.ora_precal.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p]
         L.ora_get_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
+        L.ora_get_all_sad.argtypes = L.ora_get_disp.argtypes
         L.ora_get_disp.restype = ctypes.c_int
         L.ora_box_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _i32p, _u32p]
         L.ora_box_disp.restype = ctypes.c_int
@@ -120,6 +121,19 @@ def get_disp(left, right, sad_window_size: int, search_range: int) -> np.ndarray
     rc = lib().ora_get_disp(_p(left, _u8p), _p(right, _u8p), W, H, sad_window_size, search_range, _p(out, _u8p), None)
     if rc != 0:
         raise MemoryError("ora_get_disp")
+    return out
+
+
+def get_all_sad(left, right, sad_window_size: int, search_range: int) -> np.ndarray:
+    """Literal restatement of ``getAllSAD`` (BlockMatching.cpp:191-261): uint8 [H, W, D] (pixel-major
+    ``data_dm[p * D + d]``), each window SAD truncated to uchar, 255 where col + d > W."""
+    left, right = _img(left), _img(right)
+    H, W = left.shape
+    out = np.empty((H, W, search_range), np.uint8)
+    rc = lib().ora_get_all_sad(_p(left, _u8p), _p(right, _u8p), W, H, sad_window_size, search_range,
+                               _p(out, _u8p), None)
+    if rc != 0:
+        raise MemoryError("ora_get_all_sad")
     return out
 
 

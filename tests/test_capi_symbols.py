@@ -106,3 +106,17 @@ def test_host_alloc_rejects_bad_args():
     p = ctypes.c_void_p()
     assert L.sm_host_alloc(0, ctypes.byref(p)) != 0 and not p.value
     assert L.sm_host_free(None) == 0
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc absent")
+def test_addtid_stores_follow_their_own_m0_write():
+    """ds_write_addtid_b32 addresses LDS through M0.  Each such store must sit in the asm statement
+    that writes M0 (s_mov_b32 m0 + s_nop 0 right before it), so no compiler-generated M0
+    use can fall between the write and the store (tools/check_lds_barriers.py --m0 on the ISA)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("check_lds_barriers",
+                                                  os.path.join(ROOT, "tools", "check_lds_barriers.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    total, bad = mod.check(os.path.join(ROOT, "gpu_stereo_matching_amd", "csrc", "bm_guided.hip"), m0=True)
+    assert total > 0 and bad == 0, f"{bad} of {total} add-TID stores are not behind their own M0 write"

@@ -54,3 +54,25 @@ def test_plan_emulated_collectives_equal_full_range(n, W, H, r, D):
     for k in range(n):
         out[k * chunk:(k + 1) * chunk] = sharding.keys_to_disparity_host(red[k * chunk:(k + 1) * chunk], r)
     assert np.array_equal(out[:P].reshape(H, W), O.box_disp(L, R, r, D))
+
+
+@pytest.mark.parametrize("n", range(1, 9))
+@pytest.mark.parametrize("P,D", [(1, 1), (37 * 23, 37), (37 * 23, 5), (1920 * 1080, 256), (7, 300)])
+def test_python_twin_equals_library(n, P, D):
+    """sharding.dslice_plan_py (used where libsm_hip.so is not built) gives sm_dslice_plan's numbers."""
+    for k in range(n):
+        assert sharding.dslice_plan_py(P, D, k, n) == sharding.dslice_plan(P, D, k, n)
+    with pytest.raises(ValueError):
+        sharding.dslice_plan_py(0, 8, 0, 2)
+
+
+def test_plan_without_library(monkeypatch):
+    """A process without the HIP build still gets the plan (pure-Python twin), not an ImportError."""
+    from gpu_stereo_matching_amd import _capi
+
+    def missing(*a, **k):
+        raise ImportError("libsm_hip.so not built")
+    monkeypatch.setattr(_capi, "load", missing)
+    assert sharding.dslice_plan(100, 64, 1, 4) == (16, 32, 25, 100)
+    assert sharding.dslice_bounds(64, 3, 4) == (48, 64)
+    assert sharding.padded_pixels(10, 10, 8) == 104

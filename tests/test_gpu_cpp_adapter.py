@@ -60,10 +60,22 @@ def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):
     _write_pgm(tmp_path / "l.pgm", gray[f"{pair}/view1"])
     _write_pgm(tmp_path / "r.pgm", gray[f"{pair}/view5"])
     env = dict(os.environ, SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
-               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD=str(sad), SM_RANGE=str(rng), SM_VERBOSE="1")
+               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD=str(sad), SM_RANGE=str(rng))
+    env.pop("SM_QUIET", None)
     r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert "GPU : " in r.stdout and "find corr : " in r.stdout
+    # Device.cu:218,238,257,292: the four stage lines, in order, always printed (ms; the upload, match
+    # and download times are the recorded hipEvent split, "pre calculation" is fused and reads 0)
+    lines = r.stdout.splitlines()
+    labels = [ln.split(" : ")[0] for ln in lines if " : " in ln]
+    assert labels[:4] == ["upload data", "pre calculation", "find corr", "download data"], r.stdout
+    vals = {ln.split(" : ")[0]: float(ln.split(" : ")[1]) for ln in lines[:4]}
+    assert vals["upload data"] > 0 and vals["find corr"] > 0 and vals["download data"] > 0
+    assert vals["pre calculation"] == 0
+    assert "GPU : " in r.stdout
+    env["SM_QUIET"] = "1"
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "find corr" not in r.stdout
     got = _read_pgm(tmp_path / "d.pgm")
     assert np.array_equal(got, bm_expected[f"{pair}/r{sad}/D{rng}"])
 
@@ -141,19 +153,52 @@ def test_cvtcolor_test_cpp(tmp_path, gray, oracle):
     assert np.array_equal(got, gray["Art_/view1"])
 
 
+def _sections(stdout: str):
+    """stdout of blockMatchingApiTest split at its "== name" markers -> {name: [lines]}"""
+    out, cur = {}, None
+    for ln in stdout.splitlines():
+        if ln.startswith("== "):
+            cur = ln[3:]
+            out[cur] = []
+        elif cur is not None and ln:
+            out[cur].append(ln)
+    return out
+
+
 @pytest.mark.gpu
-def test_blockmatching_h_api_cpp(tmp_path, gray, bm_expected, oracle):
-    """testBM / getDisp / PreCal (BlockMatching.h:8-10) through stereo_bm.hpp."""
-    L, R = gray["Art/view1"], gray["Art/view5"]
+@pytest.mark.parametrize("pair,sad", [("Art", 3), ("Books", 9)])
+def test_blockmatching_h_api_cpp(tmp_path, gray, bm_expected, oracle, pair, sad):
+    """All seven BlockMatching.h functions (BlockMatching.h:8-15) through stereo_bm.hpp, in one C++
+    caller: testBM / getDisp maps and the PreCal volume against the oracle, getAllSAD's pixel-major
+    uchar volume bit-exact against ora_get_all_sad (BlockMatching.cpp:191-261; r = 9 takes the direct
+    kernel, r = 3 the volume + transpose path), and compareDiff / compareDisp / compareSAD printing
+    the reference's format (BlockMatching.cpp:263-308): nothing but "-1" on the computed results, and
+    exactly the planted index on a corrupted copy."""
+    L, R = gray[f"{pair}/view1"], gray[f"{pair}/view5"]
+    H, W = L.shape
     _write_pgm(tmp_path / "l.pgm", L)
     _write_pgm(tmp_path / "r.pgm", R)
     env = dict(os.environ, SM_DEMO="blockMatchingApiTest", SM_LEFT=str(tmp_path / "l.pgm"),
-               SM_RIGHT=str(tmp_path / "r.pgm"), SM_SAD="3", SM_RANGE="64", SM_OUT=str(tmp_path / "a.pgm"),
-               SM_OUT2=str(tmp_path / "b.pgm"), SM_VOL=str(tmp_path / "v.u8"))
-    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+               SM_RIGHT=str(tmp_path / "r.pgm"), SM_SAD=str(sad), SM_RANGE="64", SM_OUT=str(tmp_path / "a.pgm"),
+               SM_OUT2=str(tmp_path / "b.pgm"), SM_VOL=str(tmp_path / "v.u8"), SM_SADVOL=str(tmp_path / "s.u8"))
+    env.pop("SM_QUIET", None)
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    want = bm_expected["Art/r3/D64"]
+    want = bm_expected[f"{pair}/r{sad}/D64"] if f"{pair}/r{sad}/D64" in bm_expected else oracle.box_disp(L, R, sad, 64)
     assert np.array_equal(_read_pgm(tmp_path / "a.pgm"), want)
     assert np.array_equal(_read_pgm(tmp_path / "b.pgm"), want)
-    vol = np.fromfile(tmp_path / "v.u8", np.uint8).reshape(64, *L.shape)
+    vol = np.fromfile(tmp_path / "v.u8", np.uint8).reshape(64, H, W)
     assert np.array_equal(vol, oracle.precal(L, R, 64))
+    allsad = np.fromfile(tmp_path / "s.u8", np.uint8).reshape(H, W, 64)
+    assert np.array_equal(allsad, oracle.get_all_sad(L, R, sad, 64))
+    sec = _sections(r.stdout)
+    # BlockMatching.cpp's step lines around each call (getDisp inside compareDisp prints them too)
+    assert "main loop" in r.stdout and "precalculate diff" in r.stdout and "prep location" in r.stdout
+    assert sec["compareDiff clean"] == ["-1"]
+    assert [ln for ln in sec["compareDisp clean"] if ln.startswith(("[", "CPU"))] == []
+    assert [ln for ln in sec["compareSAD clean"] if not ln.startswith(("prep", "precalculate"))] == ["-1"]
+    assert sec["compareDiff planted"] == ["7", "-1"]
+    d = int(want[1, 2])
+    assert [ln for ln in sec["compareDisp planted"] if ln.startswith(("[", "CPU"))] == \
+        ["[1:2]", f"CPU = {d}, GPU = {d ^ 1}"]
+    assert [ln for ln in sec["compareSAD planted"] if not ln.startswith(("prep", "precalculate"))] == ["5", "-1"]

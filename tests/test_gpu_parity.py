@@ -384,21 +384,72 @@ def test_error_codes_side_entries(sm, torch):
     small.close()
 
 
-def test_stage_timings(matcher, gray, oracle):
+def test_stage_timings(sm, gray, oracle):
+    """SM_PARAM_STAGE_TIMING: auto (default) records the upload / match / download split from the
+    first sm_last_stage_ms read on (the drop-in call skips the two hipEvent markers until someone
+    reads the split); 1 always; 0 never (the split reads 0).  Maps never change."""
     L, R = gray["Art_/view1"], gray["Art_/view5"]
-    want = matcher.match(L, R, 5, 64)
-    u, c, d = matcher.stage_ms()
-    assert u > 0 and c > 0 and d > 0
-    # SM_PARAM_STAGE_TIMING 0: no stage events, the split reads 0, the map is unchanged
-    matcher.set_stage_timing(False)
-    try:
-        assert np.array_equal(matcher.match(L, R, 5, 64), want)
-        assert matcher.stage_ms() == (0.0, 0.0, 0.0)
-    finally:
-        matcher.set_stage_timing(True)
-    matcher.match(L, R, 5, 64)
-    assert min(matcher.stage_ms()) > 0
+    with sm.BlockMatcher(0, 640, 480, 256) as m:
+        want = m.match(L, R, 5, 64)
+        assert m.stage_ms() == (0.0, 0.0, 0.0)      # auto: not recorded before the first read
+        assert np.array_equal(m.match(L, R, 5, 64), want)
+        u, c, d = m.stage_ms()                       # armed by the first read
+        assert u > 0 and c > 0 and d > 0
+        m.set_stage_timing(False)
+        assert np.array_equal(m.match(L, R, 5, 64), want)
+        assert m.stage_ms() == (0.0, 0.0, 0.0)
+        m.set_stage_timing(True)
+        m.match(L, R, 5, 64)
+        assert min(m.stage_ms()) > 0
+        m.set_stage_timing("auto")                   # already armed on this handle
+        m.match(L, R, 5, 64)
+        assert min(m.stage_ms()) > 0
     assert np.array_equal(want, oracle.box_disp(L, R, 5, 64))
+
+
+@pytest.mark.parametrize("pair,r,D", [("Art_", 5, 64), ("Art", 4, 64), ("Books", 3, 64), ("Dolls", 9, 64)])
+def test_all_sad_golden_pairs(matcher, gray, oracle, pair, r, D):
+    """getAllSAD (BlockMatching.cpp:191-261) bit-exact with its literal restatement ora_get_all_sad:
+    pixel-major [p*D + d], uchar truncation of every window SAD, 255 where col + d > cols.  r <= 7
+    runs AD volume -> u16 SAD volume -> transpose; r = 9 the direct kernel."""
+    L, R = gray[f"{pair}/view1"], gray[f"{pair}/view5"]
+    got = matcher.all_sad(L, R, r, D)
+    assert got.shape == (*L.shape, D)
+    assert np.array_equal(got, oracle.get_all_sad(L, R, r, D))
+
+
+@pytest.mark.parametrize("W,H,r,D", [(1, 1, 0, 1), (5, 3, 1, 7), (40, 9, 0, 64), (65, 33, 7, 129), (33, 50, 2, 256),
+                                     (200, 17, 8, 30), (31, 12, 15, 20), (4100, 3, 2, 9)])
+def test_all_sad_shapes(matcher, oracle, torch, W, H, r, D):
+    """getAllSAD on odd shapes: W < D (most entries 255), D = 1 / 256, r = 0 and r up to 15 (the
+    direct kernel), W > 4096 (beyond the AD-volume kernel: the direct kernel); host and device forms
+    equal."""
+    rng = np.random.default_rng(W * 7 + H * 13 + r + D)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    want = oracle.get_all_sad(L, R, r, D)
+    if W <= matcher.max_width:   # the host form stages through the handle's frames
+        assert np.array_equal(matcher.all_sad(L, R, r, D), want)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    out = matcher.all_sad_device(Lt, Rt, r, D)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_all_sad_1080p(matcher, torch):
+    """getAllSAD at 1080p D=128 r=5 (265 MB volume): the device form against the u16 SAD volume's low
+    bytes (itself checked against the oracle in test_sad_volume), with the 255 rule."""
+    from gpu_stereo_matching_amd import synth
+    L, R = synth.synth_pair(1234, 1920, 1080, 128)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    vol = matcher.sad_volume_device(Lt, Rt, 5, 128)
+    allsad = matcher.all_sad_device(Lt, Rt, 5, 128)
+    low = (vol.to(torch.int32) & 0xFF).permute(1, 2, 0)
+    x = torch.arange(1920, device="cuda").view(1, 1920, 1)
+    d = torch.arange(128, device="cuda").view(1, 1, 128)
+    want = torch.where(x + d > 1920, torch.full_like(low, 255), low).to(torch.uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(allsad, want)
 
 
 def test_frame_stream_pipeline(matcher, oracle, torch):

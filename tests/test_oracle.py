@@ -251,3 +251,31 @@ def test_st2_pipeline_pieces(oracle):
     t = oracle.st_tree_depth(L, l1, mk, 16)
     assert t["levels"] > 0 and sorted(t["node"].tolist()) == list(range(H * W))
     assert (out[:, 12:] == s).mean() > 0.97
+
+
+@pytest.mark.parametrize("H,W,r,D", [(20, 33, 2, 16), (17, 9, 3, 12), (5, 40, 0, 40), (30, 50, 5, 8), (6, 7, 9, 10)])
+def test_get_all_sad_two_restatements(oracle, H, W, r, D):
+    """getAllSAD (BlockMatching.cpp:191-261): the literal loop nest (ora_get_all_sad) equals the
+    separable box-sum volume (ora_box_cost) transposed to pixel-major, truncated to uchar, with 255
+    where col + d > cols — including W < D and r larger than the frame."""
+    rng = np.random.default_rng(H * W + r * 31 + D)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    got = oracle.get_all_sad(L, R, r, D)
+    low = (oracle.box_cost(L, R, r, D).transpose(1, 2, 0) & 0xFF).astype(np.uint8)
+    x = np.arange(W)[None, :, None]
+    d = np.arange(D)[None, None, :]
+    assert np.array_equal(got, np.where(x + d > W, 255, low).astype(np.uint8))
+
+
+def test_get_all_sad_golden_pair(oracle, gray):
+    """On the bundled Art_ pair at singleFrame's configuration (r = 5, D = 64): every valid entry is
+    the low byte of the box SAD, every entry with col + d > cols is 255."""
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    vol = oracle.get_all_sad(L, R, 5, 64)
+    full = oracle.box_cost(L, R, 5, 64).transpose(1, 2, 0)
+    x = np.arange(L.shape[1])[None, :, None]
+    d = np.arange(64)[None, None, :]
+    valid = np.broadcast_to(x + d <= L.shape[1], vol.shape)
+    assert np.array_equal(vol[valid], (full[valid] & 0xFF).astype(np.uint8))
+    assert (vol[~valid] == 255).all()

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build a libsm_hip.so variant for same-box A/B timing: tools/build_variant.sh NAME "-DFOO=1 ..."
-# -> tools/ab/NAME.so (objects under tools/ab/NAME/).  Not part of the product build.
+# -> tools/abv/NAME.so (objects under tools/abv/NAME/).  Not part of the product build.
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 EXTRA="$*"
-SRC=gpu_stereo_matching_amd/csrc
-OUT=tools/ab/$NAME
+SRC=${SM_VARIANT_SRC:-gpu_stereo_matching_amd/csrc}
+OUT=tools/abv/$NAME
 mkdir -p $OUT
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wall -Wno-unused-result $EXTRA"
 pids=()
@@ -15,5 +15,5 @@ for f in sm_capi bm_box bm_aux bm_guided bm_segtree bm_pre bm_post bm_volume bm_
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ab/$NAME.so $OUT/*.o
-echo built tools/ab/$NAME.so
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/abv/$NAME.so $OUT/*.o
+echo built tools/abv/$NAME.so
