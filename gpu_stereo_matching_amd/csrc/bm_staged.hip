@@ -38,6 +38,14 @@ constexpr int kSO = kSC - 16;      // K2: output columns per strip (the strip st
 #define SM_SAD_PF 1   // next row group in flight: 154.6 vs 156.8 us per frame (same box, 5 rounds)
 #endif
 constexpr int kSadBlocks = SM_SAD_BLOCKS;  // K2 blocks per launch (>= 32-row bands)
+// K2 walking direction (round 4): odd bands walk their rows bottom-up, so the 2r halo
+// rows two neighbouring bands share are read by both at the same phase of their walks (both at the
+// start, or both at the end) while they run side by side on one XCD: the second read hits that XCD's
+// L2.  With every band walking down, band b read its top halo at its start and band b - 1 the same
+// rows at its end, ~12 MB of XCD traffic later (4 MB L2): rocprof counted 1.046x the algorithmic bytes.
+#ifndef SM_SAD_ZIGZAG
+#define SM_SAD_ZIGZAG 1
+#endif
 static_assert(kCPT == 4 || kCPT == 8, "K2 columns per thread");
 
 // K2: one column strip x one row band of one d plane per block.  A thread owns kCPT input columns
@@ -65,6 +73,10 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
     const int yo0 = band * rows_per_band;
     const int yo1 = min(H, yo0 + rows_per_band);
     if (yo0 >= H) return;                               // block-uniform
+    // the walk runs over virtual rows v; image row phys(v) reflects the band's input range
+    // [yo0 - R, yo1 + R) (and its output rows [yo0, yo1)) onto itself for a bottom-up band
+    const bool up = SM_SAD_ZIGZAG && (band & 1);
+    auto phys = [&](int v) { return up ? yo0 + yo1 - 1 - v : v; };
     const int64_t P = (int64_t)W * H;
     const uint8_t* plane = ad + (int64_t)d * P;
     uint16_t* outp = sad + (int64_t)d * P;
@@ -112,7 +124,7 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
             res[k] = sum;                               // <= (2r+1)^2 * 255 < 2^16 for r <= 7
         }
         if (out_on) {
-            uint16_t* dst = outp + (int64_t)y * W + x;
+            uint16_t* dst = outp + (int64_t)phys(y) * W + x;
             if (vec_out && x + kCPT <= W) {
                 if constexpr (kCPT == 8) {
                     const u32x4 v = {res[0] | (res[1] << 16), res[2] | (res[3] << 16), res[4] | (res[5] << 16),
@@ -147,8 +159,8 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
     auto load_group = [&](int base, Words<NG>* nw) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const int y = base + j;
-            const bool ok = col_in && y >= 0 && y < H && y < yi_end;
+            const int y = phys(base + j);
+            const bool ok = col_in && y >= 0 && y < H && base + j < yi_end;
             const uint32_t off = ok ? (uint32_t)(y * W + xin) : 0x80000000u;
             if constexpr (kCPT == 8) {
                 uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(prs, off, 0, 0));
