@@ -822,7 +822,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     // tree on the host
     const auto t0 = std::chrono::steady_clock::now();
     HostTree t;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 1.0f, t)) return hipErrorInvalidValue;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t)) return hipErrorInvalidValue;
     float table[256];
     weight_table(sigma, table);
     const float tree_ms = ms_since(t0);
@@ -898,14 +898,14 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // be destroyed): a failed build reports false
     std::thread th([&] {
         try {
-            okR = tree_from_edges(static_cast<Edge*>(ws.h_edges[1]), nE, (int)P, tau, 1.0f, tr);
+            okR = tree_from_edges(static_cast<Edge*>(ws.h_edges[1]), nE, (int)P, W, tau, 1.0f, tr);
         } catch (...) {
             okR = false;
         }
     });
     bool okL = false;
     try {
-        okL = tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 1.0f, tl);
+        okL = tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, tl);
     } catch (...) {
         okL = false;
     }
@@ -951,7 +951,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(hipStreamSynchronize(s));
     t0 = std::chrono::steady_clock::now();
     HostTree td;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, tau, 255.0f, td)) return hipErrorInvalidValue;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td)) return hipErrorInvalidValue;
     float tab2[256];
     weight_table(sigma, tab2);
     tree_ms += ms_since(t0);

@@ -20,38 +20,6 @@ namespace sm {
 namespace st_host {
 
 // ---- host: the tree (sequential, as the reference's) ----
-// disjoint-set.h's forest as separate arrays: find walks only the parent array (a packed 16-B record
-// per element measured 25 % slower on the Art tree)
-struct Dsu {
-    std::vector<int> p, rank, size;
-    explicit Dsu(int n) : p(n), rank(n, 0), size(n, 1) {
-        for (int i = 0; i < n; ++i) p[i] = i;
-    }
-    // disjoint-set.h:58-64 walks to the root and points x at it.  Path halving here: compression moves
-    // only non-root parent pointers, so every root, rank and size (all that join and segment_graph
-    // read) is the reference's; the walks are shorter.
-    int find(int x) {
-        while (x != p[x]) {
-            p[x] = p[p[x]];
-            x = p[x];
-        }
-        return x;
-    }
-    void join(int x, int y) {   // disjoint-set.h:66-82
-        if (x != p[x]) x = find(x);
-        if (y != p[y]) y = find(y);
-        if (x == y) return;
-        if (rank[x] > rank[y]) {
-            p[y] = x;
-            size[x] += size[y];
-        } else {
-            p[x] = y;
-            size[y] += size[x];
-            if (rank[x] == rank[y]) rank[y]++;
-        }
-    }
-};
-
 struct HostTree {
     std::vector<int> node, rank, parent, first, lev;
     std::vector<uint8_t> pdist;
@@ -110,54 +78,82 @@ std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P)
 }
 
 // BuildSegmentTree (SegmentTree.cpp:38-139) from the nE sorted edges e (consumed: the cross-segment
-// penalty is added in place): segment_graph, the neighbour
-// lists with dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255 colour + depth),
-// BFS from pixel 0, level by level.
-bool tree_from_edges(Edge* e, int nE, int P, float tau, float wscale, HostTree& t) {
+// penalty is added in place) of a W-wide image: segment_graph, the neighbour lists with
+// dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255 colour + depth), BFS from
+// pixel 0, level by level.
+// Round 4 (same trees bit for bit, tests/test_st_host.py): a root's size, rank and threshold in one
+// record (they are read together at every join); the second segment_graph pass skips the edges the
+// first one joined (their ends already share a root) and appends each marked edge to the neighbour
+// lists as it goes, which is the sorted-edge order of SegmentTree.cpp:74-95 without a third pass; the
+// lists are 8 B per pixel (four distances, four 2-bit directions, the count) instead of 24.
+bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
 SM_ST_NO_CONTRACT
-    // segment_graph (segment-graph.h:48-101)
-    Dsu u(P);
-    std::vector<float> thr(P, tau / 1);
+    // segment_graph (segment-graph.h:48-101) on disjoint-set.h's forest (Dsu's rules, roots packed)
+    std::vector<int> par(P);
+    for (int i = 0; i < P; ++i) par[i] = i;
+    struct Root {
+        float thr;   // segment-graph.h:63 threshold, tau / 1 at the start
+        int size, rank;
+    };
+    std::vector<Root> R(P, Root{tau / 1, 1, 0});
+    auto find = [&](int x) {   // path halving, as Dsu::find
+        while (x != par[x]) {
+            par[x] = par[par[x]];
+            x = par[x];
+        }
+        return x;
+    };
+    auto join = [&](int x, int y) {   // disjoint-set.h:66-82 on roots x != y; returns the new root
+        if (R[x].rank > R[y].rank) {
+            par[y] = x;
+            R[x].size += R[y].size;
+            return x;
+        }
+        par[x] = y;
+        R[y].size += R[x].size;
+        if (R[x].rank == R[y].rank) R[y].rank++;
+        return y;
+    };
     std::vector<uint8_t> mask(nE, 0);
     for (int i = 0; i < nE; ++i) {
-        int a = u.find(e[i].a), b = u.find(e[i].b);
-        if (a != b && e[i].w <= thr[a] && e[i].w <= thr[b]) {
+        const int a = find(e[i].a), b = find(e[i].b);
+        if (a != b && e[i].w <= R[a].thr && e[i].w <= R[b].thr) {
             mask[i] = 1;
-            u.join(a, b);
-            a = u.find(a);
-            thr[a] = e[i].w + tau / u.size[a];
+            const int r = join(a, b);
+            R[r].thr = e[i].w + tau / R[r].size;
         }
     }
+    // neighbour lists: direction k of pixel p is (dir >> 2k) & 3 -> offset -1, +1, -W, +W
+    struct Adj {
+        uint32_t d;
+        uint16_t dir, n;
+    };
+    std::vector<Adj> adj(P, Adj{0u, 0, 0});
+    auto link = [&](int pa, int pb, uint8_t dis) {
+        const int diff = pb - pa;
+        const uint32_t da = diff == -1 ? 0u : diff == 1 ? 1u : diff < 0 ? 2u : 3u;
+        Adj& A = adj[pa];
+        A.d |= (uint32_t)dis << (8 * A.n);
+        A.dir |= (uint16_t)(da << (2 * A.n));
+        A.n++;
+        Adj& B = adj[pb];
+        B.d |= (uint32_t)dis << (8 * B.n);
+        B.dir |= (uint16_t)((da ^ 1u) << (2 * B.n));
+        B.n++;
+    };
     for (int i = 0; i < nE; ++i) {
-        const int a = u.find(e[i].a), b = u.find(e[i].b);
-        if (a != b) {
-            const int size_min = std::min(u.size[a], u.size[b]);
-            u.join(a, b);
-            mask[i] = 1;
+        if (!mask[i]) {   // segment-graph.h:88-99: join the remaining components
+            const int a = find(e[i].a), b = find(e[i].b);
+            if (a == b) continue;
+            const int size_min = std::min(R[a].size, R[b].size);
+            join(a, b);
             if (size_min > 50) e[i].w += 5;   // MIN_SIZE_SEG, PENALTY_CROSS_SEG
         }
-    }
-    // neighbour lists in sorted-edge order (SegmentTree.cpp:74-95), one 24-B record per pixel
-    struct Adj {
-        int q[4];
-        uint8_t d[4];
-        int n;
-    };
-    std::vector<Adj> adj(P);
-    for (int p = 0; p < P; ++p) adj[p].n = 0;
-    for (int i = 0; i < nE; ++i) {
-        if (!mask[i]) continue;
-        const int pa = e[i].a, pb = e[i].b;
         const float sw = e[i].w * wscale;
-        const uint8_t dis = (uint8_t)std::min((int)(sw + 0.5f), 255);
-        Adj& A = adj[pa];
-        A.q[A.n] = pb;
-        A.d[A.n++] = dis;
-        Adj& B = adj[pb];
-        B.q[B.n] = pa;
-        B.d[B.n++] = dis;
+        link(e[i].a, e[i].b, (uint8_t)std::min((int)(sw + 0.5f), 255));
     }
     // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level
+    const int off[4] = {-1, 1, -W, W};
     t.node.assign(P, 0);
     t.rank.assign(P, 0);
     t.parent.assign(P, -1);
@@ -177,12 +173,12 @@ SM_ST_NO_CONTRACT
             t.rank[p] = i;
             t.first[i] = end;
             uint32_t ch = 0, n = 0;
-            const Adj& A = adj[p];
+            const Adj A = adj[p];
             for (int k = 0; k < A.n; ++k) {
-                const int q = A.q[k];
+                const int q = p + off[(A.dir >> (2 * k)) & 3];
                 if (q == pp) continue;
                 ppix[end] = p;
-                const uint8_t dis = A.d[k];
+                const uint8_t dis = (uint8_t)(A.d >> (8 * k));
                 ch |= (uint32_t)dis << (8 * (n + 1));
                 ++n;
                 t.node[end] = q;
@@ -198,7 +194,7 @@ SM_ST_NO_CONTRACT
 
 bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
     std::vector<Edge> e = sorted_edges_u8(wr, wu, W, W * H);
-    return tree_from_edges(e.data(), (int)e.size(), W * H, tau, 1.0f, t);
+    return tree_from_edges(e.data(), (int)e.size(), W * H, W, tau, 1.0f, t);
 }
 
 // CColorDepthWeight::GetWeight (SegmentTree.cpp:204-219) from the colour weights (max channel |diff| on

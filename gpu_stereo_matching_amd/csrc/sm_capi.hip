@@ -635,17 +635,25 @@ int group_comms(sm_group* g) {
 // (Device.cu:43-61: the d planes are independent); the P keys are padded with the "no match" key to
 // Ppad = n * chunk so that the MIN reduce-scatter hands member k the pixels [k*chunk, (k+1)*chunk),
 // and the all-gather puts chunk k back at offset k*chunk.
+// The pair itself is split by rows (round 4): member k uploads only image rows
+// [k*rows_per, (k+1)*rows_per) of each frame over its own PCIe link, into slot k of an n*rows_per-row
+// buffer, and an in-place RCCL all-gather over xGMI assembles both frames on every member before the
+// key pass.  No halo is needed: the gathered frames are the whole pair.
 struct DslicePlan {
     int lo, hi;
     int64_t chunk, padded;
+    int rows_per, row_lo, row_hi;   // this member's upload rows [row_lo, row_hi) (empty past the frame)
 };
 
-DslicePlan dslice_plan(int64_t P, int D, int n, int k) {
+DslicePlan dslice_plan(int64_t P, int D, int n, int k, int H = 1) {
     DslicePlan p;
     p.lo = (int)((int64_t)k * D / n);
     p.hi = (int)((int64_t)(k + 1) * D / n);
     p.chunk = (P + n - 1) / n;
     p.padded = p.chunk * n;
+    p.rows_per = (H + n - 1) / n;
+    p.row_lo = std::min(H, k * p.rows_per);
+    p.row_hi = std::min(H, (k + 1) * p.rows_per);
     return p;
 }
 
@@ -672,9 +680,9 @@ bool dslice_fault(int k, const char* phase) {
 }
 
 // Member-side key pass over its slice: keys[0, padded) on stream s from the frames already on the
-// device (d_left / d_right, pitch W).
-int dslice_keys(sm_handle* h, const DslicePlan& p, int W, int H, int radius, bool guided, uint32_t* keys,
-                hipStream_t s) {
+// device (dL / dR, pitch W).
+int dslice_keys(sm_handle* h, const DslicePlan& p, const uint8_t* dL, const uint8_t* dR, int W, int H, int radius,
+                bool guided, uint32_t* keys, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
     const uint32_t none = dslice_none_key(radius, guided);
     if (p.padded > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(p.padded - P), s));
@@ -683,13 +691,13 @@ int dslice_keys(sm_handle* h, const DslicePlan& p, int W, int H, int radius, boo
         return SM_OK;
     }
     if (guided) {
-        SM_HIP(sm::launch_guided_slice_keys(h->d_left, h->d_right, W, H, W, 1, P, radius, p.lo, p.hi, h->guided_eps,
+        SM_HIP(sm::launch_guided_slice_keys(dL, dR, W, H, W, 1, P, radius, p.lo, p.hi, h->guided_eps,
                                             reinterpret_cast<int*>(keys), s));
         return SM_OK;
     }
     sm::MatchArgs a{};
-    a.left = h->d_left;
-    a.right = h->d_right;
+    a.left = dL;
+    a.right = dR;
     a.W = W;
     a.H = H;
     a.pitch = W;
@@ -714,38 +722,64 @@ int dslice_finalise(const uint32_t* mine, int64_t chunk, int radius, bool guided
     return SM_OK;
 }
 
-// Member workspace: keys [padded] | reduced chunk [chunk] | uint8 chunk [chunk] | gathered map [padded]
+// Member workspace: keys [padded] | reduced chunk [chunk] | uint8 chunk [chunk] | gathered map [padded] |
+// gathered left frame [n * rows_per * W] | gathered right frame [same]  (each region 256-B aligned)
 struct DsliceWs {
     uint32_t* keys;
     uint32_t* mine;
     uint8_t* mine8;
     uint8_t* map;
+    uint8_t* gl;
+    uint8_t* gr;
+    int64_t slot;   // bytes of one member's row slot (rows_per * W)
+    size_t bytes;
 };
-DsliceWs dslice_ws(sm_handle* h, const DslicePlan& p) {
+inline int64_t a256(int64_t v) { return (v + 255) & ~(int64_t)255; }
+DsliceWs dslice_ws(uint8_t* base, const DslicePlan& p, int n, int W) {
     DsliceWs w;
-    w.keys = reinterpret_cast<uint32_t*>(h->d_dsl);
-    w.mine = w.keys + p.padded;
-    w.mine8 = reinterpret_cast<uint8_t*>(w.mine + p.chunk);
-    w.map = w.mine8 + p.chunk;
+    w.slot = (int64_t)p.rows_per * W;
+    int64_t o = 0;
+    w.keys = reinterpret_cast<uint32_t*>(base + o);
+    o += a256(p.padded * 4);
+    w.mine = reinterpret_cast<uint32_t*>(base + o);
+    o += a256(p.chunk * 4);
+    w.mine8 = base + o;
+    o += a256(p.chunk);
+    w.map = base + o;
+    o += a256(p.padded);
+    w.gl = base + o;
+    o += a256(n * w.slot);
+    w.gr = base + o;
+    o += a256(n * w.slot);
+    w.bytes = (size_t)o;
     return w;
 }
 
-// Phase 1 of member k (its worker thread): workspace, upload, slice keys, and a stream sync so that
-// every local failure (allocation, copy, launch, kernel fault) is known before any member enqueues a
-// collective.  A member that fails here returns before phase 2 starts, so nobody waits on it.
-int dslice_member_keys(sm_handle* h, int k, int n, const uint8_t* left, const uint8_t* right, int W, int H, int pitch,
-                       int radius, int D, bool guided) {
+// Member k's rows of the pair into its slot of the gathered frames (host -> device, its own PCIe link).
+int dslice_upload_rows(const DslicePlan& p, const DsliceWs& w, int k, const uint8_t* left, const uint8_t* right, int W,
+                       int pitch, hipStream_t s) {
+    const int nr = p.row_hi - p.row_lo;
+    if (nr <= 0) return SM_OK;   // a member past the frame's last row contributes a pad slot only
+    const int64_t off = (int64_t)p.row_lo * pitch;
+    SM_HIP(copy2d(w.gl + k * w.slot, W, left + off, pitch, W, nr, hipMemcpyHostToDevice, s));
+    SM_HIP(copy2d(w.gr + k * w.slot, W, right + off, pitch, W, nr, hipMemcpyHostToDevice, s));
+    return SM_OK;
+}
+
+// Phase 1 of member k (its worker thread): workspace and the upload of its rows, then a stream sync
+// so that every local failure (allocation, copy) is known before any member enqueues a collective.  A
+// member that fails here returns before phase 2 starts, so nobody waits on it.
+int dslice_member_upload(sm_handle* h, int k, int n, const uint8_t* left, const uint8_t* right, int W, int H,
+                         int pitch, int D) {
     const int64_t P = (int64_t)W * H;
-    const DslicePlan p = dslice_plan(P, D, n, k);
+    const DslicePlan p = dslice_plan(P, D, n, k, H);
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
     if (dslice_fault(k, "keys")) return fail(SM_ERR_LAUNCH, "d-slice member %d: injected fault (keys)", k);
-    int rc = ensure_dsl(h, (size_t)(p.padded * 4 + p.chunk * 4 + p.chunk + p.padded));
+    int rc = ensure_dsl(h, dslice_ws(nullptr, p, n, W).bytes);
     if (rc) return rc;
-    const DsliceWs w = dslice_ws(h, p);
-    SM_HIP(copy2d(h->d_left, W, left, pitch, W, H, hipMemcpyHostToDevice, s));
-    SM_HIP(copy2d(h->d_right, W, right, pitch, W, H, hipMemcpyHostToDevice, s));
-    rc = dslice_keys(h, p, W, H, radius, guided, w.keys, s);
+    const DsliceWs w = dslice_ws(h->d_dsl, p, n, W);
+    rc = dslice_upload_rows(p, w, k, left, right, W, pitch, s);
     if (rc) return rc;
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
@@ -757,15 +791,16 @@ struct DsliceSync {
     std::atomic<bool> abort{false};
 };
 
-// Phase 2 of member k: MIN reduce-scatter, finalise, all-gather, member 0 downloads.  Waits by
-// polling its stream and the shared abort flag (and RCCL's async error), so that no member blocks
-// forever on a collective a failed peer never joined (the ncclCommAbort pattern).  On any failure
-// the member's communicator is aborted and its slot set to null (the group re-creates them).
+// Phase 2 of member k: in-place all-gathers of the pair's row slots, the slice keys, MIN reduce-scatter,
+// finalise, all-gather of the map, member 0 downloads.  Waits by polling its stream and the shared abort
+// flag (and RCCL's async error), so that no member blocks forever on a collective a failed peer never
+// joined (the ncclCommAbort pattern).  On any failure the member's communicator is aborted and its slot
+// set to null (the group re-creates them).
 int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, DsliceSync* sync, int k, int n, int W,
                           int H, int radius, int D, bool guided, uint8_t* disp_out, int out_pitch) {
     const int64_t P = (int64_t)W * H;
-    const DslicePlan p = dslice_plan(P, D, n, k);
-    const DsliceWs w = dslice_ws(h, p);
+    const DslicePlan p = dslice_plan(P, D, n, k, H);
+    const DsliceWs w = dslice_ws(h->d_dsl, p, n, W);
     hipStream_t s = h->stream;
     // every failure of phase 2 goes through bail, so the others stop polling for this member
     auto bail = [&](int code, const char* what) {
@@ -776,6 +811,11 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
     };
     if (hipSetDevice(h->device) != hipSuccess) return bail(SM_ERR_LAUNCH, "hipSetDevice failed");
     if (dslice_fault(k, "collective")) return bail(SM_ERR_LAUNCH, "injected fault (collective)");
+    // the pair: every member's row slot to every member (in place: slot k is this member's send buffer)
+    if (api->all_gather(w.gl + k * w.slot, w.gl, (size_t)w.slot, ncclUint8, *comm, s) != ncclSuccess ||
+        api->all_gather(w.gr + k * w.slot, w.gr, (size_t)w.slot, ncclUint8, *comm, s) != ncclSuccess)
+        return bail(SM_ERR_LAUNCH, "ncclAllGather (pair rows) failed");
+    if (dslice_keys(h, p, w.gl, w.gr, W, H, radius, guided, w.keys, s)) return bail(SM_ERR_LAUNCH, "slice keys launch failed");
     // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
     if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, guided ? ncclInt32 : ncclUint32, ncclMin, *comm, s) !=
         ncclSuccess)
@@ -1606,12 +1646,12 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
     int rc = group_comms(g);
     if (rc) return rc;
     const int n = (int)g->w.size();
-    // phase 1 on every member: upload + slice keys, stream synchronised (no collective yet)
+    // phase 1 on every member: workspace + the upload of its rows, stream synchronised (no collective yet)
     std::vector<std::function<int()>> jobs;
     for (int k = 0; k < n; ++k) {
         sm_handle* h = g->w[k]->h;
         jobs.push_back([=]() -> int {
-            return dslice_member_keys(h, k, n, left, right, width, height, pitch, radius, num_disp, guided);
+            return dslice_member_upload(h, k, n, left, right, width, height, pitch, num_disp);
         });
     }
     rc = group_run(g, jobs);
@@ -1668,28 +1708,37 @@ SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_
         return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
     const int64_t P = (int64_t)width * height;
     const int n = members;
-    const DslicePlan p0 = dslice_plan(P, num_disp, n, 0);
-    // workspace: n members' key maps [n][padded] | uint8 map [padded]
-    rc = ensure_dsl(h, (size_t)(n * p0.padded * 4 + p0.padded));
+    const DslicePlan p0 = dslice_plan(P, num_disp, n, 0, height);
+    // workspace: one member's layout (its gathered frames are the all-gather's result, shared by every
+    // rehearsed member) followed by the other members' key maps [n - 1][padded]
+    const DsliceWs w = dslice_ws(nullptr, p0, n, width);
+    rc = ensure_dsl(h, w.bytes + (size_t)((n - 1) * p0.padded * 4));
     if (rc) return rc;
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
-    uint32_t* keys = reinterpret_cast<uint32_t*>(h->d_dsl);
-    uint8_t* map = reinterpret_cast<uint8_t*>(keys + n * p0.padded);
-    SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
-    SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
+    const DsliceWs ws = dslice_ws(h->d_dsl, p0, n, width);
+    uint32_t* extra = reinterpret_cast<uint32_t*>(h->d_dsl + w.bytes);
+    auto keys_of = [&](int k) { return k == 0 ? ws.keys : extra + (int64_t)(k - 1) * p0.padded; };
+    uint8_t* map = ws.map;
+    // the row-split upload: member k's rows into slot k of the gathered frames, which is where the
+    // in-place all-gather leaves them on every member; the pad rows of the last slots are never read
+    for (int k = 0; k < n; ++k) {
+        rc = dslice_upload_rows(dslice_plan(P, num_disp, n, k, height), ws, k, left, right, width, pitch, s);
+        if (rc) return rc;
+    }
     for (int k = 0; k < n; ++k) {   // every member's key pass, into its own buffer
-        rc = dslice_keys(h, dslice_plan(P, num_disp, n, k), width, height, radius, guided, keys + k * p0.padded, s);
+        rc = dslice_keys(h, dslice_plan(P, num_disp, n, k, height), ws.gl, ws.gr, width, height, radius, guided,
+                         keys_of(k), s);
         if (rc) return rc;
     }
     // the reduce-scatter's MIN (into member 0's buffer), then each member's chunk finalised into
     // the all-gather's slot k
     for (int k = 1; k < n; ++k)
-        SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(keys), reinterpret_cast<const int*>(keys + k * p0.padded),
+        SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.keys), reinterpret_cast<const int*>(keys_of(k)),
                                    p0.padded, s));
     for (int k = 0; k < n; ++k) {
-        const DslicePlan p = dslice_plan(P, num_disp, n, k);
-        rc = dslice_finalise(keys + k * p.chunk, p.chunk, radius, guided, map + k * p.chunk, s);
+        const DslicePlan p = dslice_plan(P, num_disp, n, k, height);
+        rc = dslice_finalise(ws.keys + k * p.chunk, p.chunk, radius, guided, map + k * p.chunk, s);
         if (rc) return rc;
     }
     SM_HIP(copy2d(disp_out, out_pitch, map, width, width, height, hipMemcpyDeviceToHost, s));

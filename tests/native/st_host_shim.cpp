@@ -31,6 +31,6 @@ extern "C" int st_host_tree_depth(const uint8_t* wr, const uint8_t* wu, const ui
     depth_weights(wr, wu, disp, mask, W, H, (float)level, fw.data(), fw.data() + P);
     std::vector<Edge> e = sorted_edges_f(fw.data(), fw.data() + P, W, P);
     HostTree t;
-    if (!tree_from_edges(e.data(), (int)e.size(), P, tau, 255.0f, t)) return -1;
+    if (!tree_from_edges(e.data(), (int)e.size(), P, W, tau, 255.0f, t)) return -1;
     return export_tree(t, P, node, parent, pdist);
 }

@@ -118,11 +118,14 @@ def test_group_dslice_rejects_repeated_device_and_flags():
 
 
 # ---- the d-slice plan for n > 1 members on one device (sm_dslice_rehearse_u8) ---------------------
-@pytest.mark.parametrize("members", [2, 3, 5, 8])
-@pytest.mark.parametrize("W,H,r,D", [(97, 31, 4, 37), (463, 370, 4, 64), (41, 19, 2, 5), (1920, 1080, 5, 256)])
+@pytest.mark.parametrize("members", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("W,H,r,D", [(97, 31, 4, 37), (463, 370, 4, 64), (41, 19, 2, 5), (1920, 1080, 5, 256),
+                                     (50, 3, 1, 16)])
 def test_dslice_rehearsal_box_bit_exact(single, members, W, H, r, D):
-    """members > 1 through the same per-member key pass, seed padding (odd P) and chunk finalisation
-    as the RCCL group call; D = 5 with 8 members gives empty slices."""
+    """members > 1 through the same per-member row-split upload (member k's rows into slot k of the
+    gathered frames, where the in-place pair all-gather leaves them), key pass, seed padding (odd P)
+    and chunk finalisation as the RCCL group call; D = 5 with 8 members gives empty slices, H = 3
+    members without rows (pad slots only)."""
     L, R = _pair(W, H, D, seed=members)
     assert np.array_equal(single.dslice_rehearse(L, R, r, D, members), single.match(L, R, r, D))
 
