@@ -92,21 +92,33 @@ constexpr uint32_t kPLow = kPOne - 1;
 #endif
 constexpr bool kGuidedRoles = SM_G_ROLES != 0;
 
-template <int R, bool ROLES = kGuidedRoles>
+// Tall tiles (round 4): 48 output rows on 6 waves instead of 32 on 4.  The P halo
+// per output drops from 64 x 52 / (44 x 32) = 2.36 to 64 x 68 / (44 x 48) = 2.06 and the A halo from
+// 1.61 to 1.48 (r = 5); the LDS plan grows to ~71 KB, so two workgroups share a CU: 12 waves, as three
+// 4-wave workgroups had.  Left-only kernel (the fused right view keeps its 32-row lane mapping).
+#ifndef SM_G_TALL
+#define SM_G_TALL 1
+#endif
+template <int R>
+constexpr bool kGuidedTall = SM_G_TALL != 0 && R >= 1 && R <= 5;
+
+template <int R, bool ROLES = kGuidedRoles, bool TALL = false>
 struct GeoF {
+    static constexpr int NT = TALL ? 384 : kT;               // threads per workgroup
+    static constexpr int NWV = NT / 64;                      // waves per workgroup
     static constexpr int TW = 64 - 4 * R;
-    static constexpr int TH = 32;
+    static constexpr int TH = TALL ? 48 : 32;
     static constexpr int AW = TW + 2 * R;
     static constexpr int AH = TH + 2 * R;
     static constexpr int PH = TH + 4 * R;
-    // phase 1 runs S1V on SV waves and S2V on the other 4 - SV (kGuidedRoles), else both on all 4
-    static constexpr int SV = ROLES ? 2 : 4;
-    static constexpr int RPS = TH / (ROLES ? 4 - SV : 4);     // output rows per S2V wave
+    // phase 1 runs S1V on SV waves and S2V on the other NWV - SV (kGuidedRoles), else both on all NWV
+    static constexpr int SV = ROLES ? NWV / 2 : NWV;
+    static constexpr int RPS = TH / (ROLES ? NWV - SV : NWV);   // output rows per S2V wave
     static constexpr int RPW = (AH + SV - 1) / SV;           // A rows per wave in S1V
     static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
     static constexpr int AHP = SV * RPW;                     // cs rows incl. the last wave's pad rows
     static constexpr int PHP = SV * RPW + 2 * R;             // staged P rows incl. pad rows (>= PH)
-    static constexpr int NSEG1 = kT / AH;                    // S1H segments per A row
+    static constexpr int NSEG1 = NT / AH;                    // S1H segments per A row
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
     static constexpr int CSS0 = (NSEG1 * SW1 + 2 * R) > 64 ? (NSEG1 * SW1 + 2 * R) : 64;
@@ -125,7 +137,8 @@ struct GeoF {
         return ((((AHP * css * 4 > PHP * 64 ? AHP * css * 4 : PHP * 64) + 15) & ~15)) + 2 * TH * MSA_ * 4 +
                AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
     }
-    static constexpr int CSS = (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : 53248)) ? CSS_B : CSS_OLD;
+    static constexpr int CSS =
+        (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : TALL ? 81920 : 53248)) ? CSS_B : CSS_OLD;
     // mm is two float planes (sum a, sum b), rows of MSA floats.  S2V stores them lane-consecutively
     // (ds_write_addtid_b32, 2 LDS cycles per 64 lanes against 6 for a float2 ds_write_b64); S2H reads
     // its segment as ds_read_b64 pairs.  MSA = 2 (mod 4): the b64 reads of 32 lanes (32 rows, one
@@ -280,13 +293,15 @@ constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && 
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
+static_assert(GeoF<5, true, true>::LDS <= 81920, "tall r = 5 tile: two workgroups per CU");
+
 // right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
 constexpr float kRightScale = 16384.0f;
 constexpr float kRightMax = 8388607.0f;    // 2^23 - 1
 constexpr float kRightMin = -8388608.0f;   // -2^23
 
-template <int R, bool RIGHT>
-__global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
+template <int R, bool RIGHT, bool TALL = false>
+__global__ __launch_bounds__((TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
@@ -298,7 +313,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // the v_fmac the f32 form gets: +0.8 % on the left-only kernel, which keeps that form; at r = 2 the
     // right view measured 409.6 -> 417.5 us/frame with it instead of its 5 spilled VGPRs, not kept)
     constexpr bool LEAN = RIGHT && ROLES;
-    using G = GeoF<R, ROLES>;
+    static_assert(!(TALL && RIGHT), "tall tiles: left-only kernel");
+    using G = GeoF<R, ROLES, TALL>;
+    constexpr int NT = G::NT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
     uint8_t* lt = smem;                                                                 // [PHP][64] (aliases cs)
@@ -322,19 +339,19 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     //      disparity d (in chunk k) reads rb[i][c + 64 - (d & 63)] ----
     auto stage_band = [&](int k) {
         const int rbase = px0 - kBandChunk * k - kBandChunk;
-        for (int e = tid; e < G::PHP * (G::RBW / 4); e += kT) {
+        for (int e = tid; e < G::PHP * (G::RBW / 4); e += NT) {
             const int i = e / (G::RBW / 4), j = e - (e / (G::RBW / 4)) * (G::RBW / 4);
             *reinterpret_cast<uint32_t*>(rb + i * G::RBW + 4 * j) = ld4(Rf, py0 + i, rbase + 4 * j, W, H, pitch);
         }
     };
     stage_band(d_lo / kBandChunk);
-    for (int e = tid; e < G::PHP * 16; e += kT) {
+    for (int e = tid; e < G::PHP * 16; e += NT) {
         const int i = e >> 4, j = e & 15;
         *reinterpret_cast<uint32_t*>(lt + i * 64 + 4 * j) = ld4(L, py0 + i, px0 + 4 * j, W, H, pitch);
     }
     __syncthreads();
     // phase-1 role of this wave: S1V strip `role` (role < SV) or S2V strip role - SV
-    const int role = ROLES ? __builtin_amdgcn_readfirstlane((wave + (int)blockIdx.x) & 3) : wave;
+    const int role = ROLES ? __builtin_amdgcn_readfirstlane((wave + (int)blockIdx.x) % G::NWV) : wave;
     const bool is_s1v = !ROLES || role < G::SV;
     // S1V state: this wave walks P rows [a0, a0 + NV) (rows past PH are pad rows that only reach
     // the pad rows of cs); lane = P column c
@@ -382,8 +399,8 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // key chain runs from each segment to the next lane: lane = segment + 8 * row.
     // With the right view, the 32-lane half-wave G = tid >> 5 holds rows {G, G + 8, G + 16, G + 24}
     // (8 segments each) so that its b64 reads of the mm planes fall on distinct bank pairs.
-    const int h2r = RIGHT ? (((tid >> 3) & 3) * 8 + (tid >> 5)) : (tid & 31);
-    const int h2s = RIGHT ? (tid & 7) : (tid >> 5);
+    const int h2r = RIGHT ? (((tid >> 3) & 3) * 8 + (tid >> 5)) : (tid % G::TH);
+    const int h2s = RIGHT ? (tid & 7) : (tid / G::TH);
     // S2H's mm row segment (plane A) as an LDS byte address; plane B is MM_PLANE bytes further
     const uint32_t h2off = (uint32_t)(G::CS_BYTES + (h2r * G::MSA + h2s * G::SW2) * 4);
     // S2V's first mm row of this wave (plane A), for the add-TID stores
@@ -766,6 +783,16 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS;
     constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && kRolesRight<R>>::LDS;
     if (!gpart) {
+        if constexpr (kGuidedTall<R>) {
+            using GT = GeoF<R, kGuidedRoles, true>;
+            const int tyt = (H + GT::TH - 1) / GT::TH;
+            const int64_t bt = (int64_t)tiles_x * tyt * batch;
+            if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((guided_fused_kernel<R, false, true>), dim3((unsigned)bt), dim3(GT::NT),
+                               (size_t)GT::LDS, s, L, Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp,
+                               out_pitch, ostride, tiles_x, tiles_x * tyt, nullptr, 0, keys);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), lds_left, s, L,
                            Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
                            tiles_x * tiles_y, nullptr, 0, keys);
