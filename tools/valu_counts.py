@@ -14,8 +14,8 @@ CTRS = "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAV
 JOBS = (
     ("box_r5_1080p_d128_b128", "box_match_kernel<5, 128, false, 4>", ["--agg", "box", "--batch", "128"],
      [1920, 1080, 128, 5, 128]),
-    ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false>", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
-    ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true>", ["--agg", "guided", "--lr", "--batch", "32"],
+    ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
+    ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true", ["--agg", "guided", "--lr", "--batch", "32"],
      [1920, 1080, 128, 5, 32]),
 )
 
