@@ -290,6 +290,12 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 #endif
 template <int R>
 constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && R <= 5 && R != 2);
+// the fused right view on tall tiles too (the radii whose right view runs the wave roles at 3 waves/SIMD)
+#ifndef SM_G_TALL_RIGHT
+#define SM_G_TALL_RIGHT 1
+#endif
+template <int R>
+constexpr bool kGuidedTallRight = SM_G_TALL_RIGHT != 0 && kGuidedTall<R> && kRolesRight<R> && R != 3;
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
@@ -313,7 +319,6 @@ __global__ __launch_bounds__((TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) v
     // the v_fmac the f32 form gets: +0.8 % on the left-only kernel, which keeps that form; at r = 2 the
     // right view measured 409.6 -> 417.5 us/frame with it instead of its 5 spilled VGPRs, not kept)
     constexpr bool LEAN = RIGHT && ROLES;
-    static_assert(!(TALL && RIGHT), "tall tiles: left-only kernel");
     using G = GeoF<R, ROLES, TALL>;
     constexpr int NT = G::NT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -397,9 +402,9 @@ __global__ __launch_bounds__((TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) v
     // S2H ownership: output row h2r, outputs [h2s*SW2, h2s*SW2 + SW2).  Rows run across lanes
     // (measured 2 % faster than segments across lanes), except with the fused right view, whose
     // key chain runs from each segment to the next lane: lane = segment + 8 * row.
-    // With the right view, the 32-lane half-wave G = tid >> 5 holds rows {G, G + 8, G + 16, G + 24}
+    // With the right view, the 32-lane half-wave G = tid >> 5 holds rows {G, G + TH/4, G + TH/2, G + 3TH/4}
     // (8 segments each) so that its b64 reads of the mm planes fall on distinct bank pairs.
-    const int h2r = RIGHT ? (((tid >> 3) & 3) * 8 + (tid >> 5)) : (tid % G::TH);
+    const int h2r = RIGHT ? (((tid >> 3) & 3) * (G::TH / 4) + (tid >> 5)) : (tid % G::TH);
     const int h2s = RIGHT ? (tid & 7) : (tid / G::TH);
     // S2H's mm row segment (plane A) as an LDS byte address; plane B is MM_PLANE bytes further
     const uint32_t h2off = (uint32_t)(G::CS_BYTES + (h2r * G::MSA + h2s * G::SW2) * 4);
@@ -732,16 +737,17 @@ __global__ __launch_bounds__(256) void guided_keys_to_disp_kernel(const int* __r
 // Right view of the fused pass: for each right pixel u of a tile row band, the minimum key over the
 // tiles whose chain emitted u (k = x0 + SPAN - 1 - u in [0, K)), decoded to d = x0 + position - u.
 // Block = 64 columns x the 32 rows of one tile band; reads are 128-B rows of gpart ([k][row]).
+template <int TH>
 __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __restrict__ gpart, int tiles_x, int tiles,
                                                                   int TW, int SPAN, int K, int W, int H,
                                                                   uint8_t* __restrict__ right, int rpitch,
                                                                   int64_t rstride) {
-    constexpr int TH = 32, UC = 64;
+    constexpr int UC = 64;
     __shared__ uint8_t band[TH][UC];
     const int u0 = blockIdx.x * UC, ty = blockIdx.y, f = blockIdx.z;
     const int* base = gpart + ((int64_t)f * tiles + (int64_t)ty * tiles_x) * K * TH;
     for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
-        const int j = e & (TH - 1), ul = e >> 5, u = u0 + ul;
+        const int j = e % TH, ul = e / TH, u = u0 + ul;
         int dr = 0;
         if (u < W) {
             const int n = u - SPAN + 1;
@@ -765,7 +771,7 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
     __syncthreads();
     uint8_t* Rf = right + (int64_t)f * rstride;
     for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
-        const int j = e >> 6, ul = e & (UC - 1);
+        const int j = e / UC, ul = e % UC;
         const int y = ty * TH + j, u = u0 + ul;
         if (y < H && u < W) Rf[(int64_t)y * rpitch + u] = band[j][ul];
     }
@@ -800,20 +806,35 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     }
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
+    if constexpr (kGuidedTallRight<R>) {
+        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, true>;
+        const int tyt = (H + GT::TH - 1) / GT::TH;
+        const int64_t bt = (int64_t)tiles_x * tyt * batch;
+        if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((guided_fused_kernel<R, true, true>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
+                           L, Rimg, W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x,
+                           tiles_x * tyt, gpart, K, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(guided_right_reduce_kernel<GT::TH>, dim3((unsigned)((W + 63) / 64), (unsigned)tyt,
+                           (unsigned)batch), dim3(256), 0, s, gpart, tiles_x, tiles_x * tyt, G::TW, span, K, W, H,
+                           right, rpitch, rstride);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), lds_right, s, L, Rimg,
                        W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
                        K, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(guided_right_reduce_kernel, dim3((unsigned)((W + 63) / 64), (unsigned)tiles_y, (unsigned)batch),
-                       dim3(256), 0, s, gpart, tiles_x, tiles_x * tiles_y, G::TW, span, K, W, H, right, rpitch,
-                       rstride);
+    hipLaunchKernelGGL(guided_right_reduce_kernel<G::TH>, dim3((unsigned)((W + 63) / 64), (unsigned)tiles_y,
+                       (unsigned)batch), dim3(256), 0, s, gpart, tiles_x, tiles_x * tiles_y, G::TW, span, K, W, H,
+                       right, rpitch, rstride);
     return hipGetLastError();
 }
 
 template <int R>
 size_t partial_bytes(int W, int H, int D, int batch) {
-    using G = GeoF<R, false>;
+    using G = GeoF<R, false, kGuidedTallRight<R>>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }
