@@ -95,9 +95,12 @@ constexpr bool kGuidedRoles = SM_G_ROLES != 0;
 // Tall tiles (round 4): 48 output rows on 6 waves instead of 32 on 4.  The P halo
 // per output drops from 64 x 52 / (44 x 32) = 2.36 to 64 x 68 / (44 x 48) = 2.06 and the A halo from
 // 1.61 to 1.48 (r = 5); the LDS plan grows to ~71 KB, so two workgroups share a CU: 12 waves, as three
-// 4-wave workgroups had.  Left-only kernel (the fused right view keeps its 32-row lane mapping).
+// 4-wave workgroups had.  Measured (round 4, same box, 1080p D=128 r=5, 32 frames per call, us per
+// frame): guided 453.3 (32-row tiles) -> 851.0 (tall), guided + LR 524.7 -> 953.2 with the right view
+// tall too (SM_G_TALL_RIGHT), no spills in either (168 / 160 VGPRs).  A dead end: off by default, kept
+// as an A/B switch (profiles/microbench/r04_guided_tall_ab.txt).
 #ifndef SM_G_TALL
-#define SM_G_TALL 1
+#define SM_G_TALL 0
 #endif
 template <int R>
 constexpr bool kGuidedTall = SM_G_TALL != 0 && R >= 1 && R <= 5;
@@ -292,7 +295,7 @@ template <int R>
 constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && R <= 5 && R != 2);
 // the fused right view on tall tiles too (the radii whose right view runs the wave roles at 3 waves/SIMD)
 #ifndef SM_G_TALL_RIGHT
-#define SM_G_TALL_RIGHT 1
+#define SM_G_TALL_RIGHT 0
 #endif
 template <int R>
 constexpr bool kGuidedTallRight = SM_G_TALL_RIGHT != 0 && kGuidedTall<R> && kRolesRight<R> && R != 3;

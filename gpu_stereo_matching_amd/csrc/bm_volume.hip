@@ -32,8 +32,14 @@ constexpr int kVT = 256;
 // back to back on one XCD and fetch those rows from its L2 once.  0: the round-3 grid (band, frame,
 // chunk) in blockIdx (x, y, z), whose chunks of one band ran ~bands*frames blocks apart: each chunk
 // re-fetched the band from the fabric (rocprof FETCH: 1.17x the algorithmic bytes per launch).
+// 2: chunk groups — the dsplit chunks in groups of SM_ADV_GC, the group's chunks fastest and XCD-contiguous,
+// then the band, then the group: the band's rows are fetched dsplit / GC times (not dsplit), while the
+// blocks in flight write GC times the planes of order 0 (fewer, longer write streams than order 1).
 #ifndef SM_ADV_ORDER
 #define SM_ADV_ORDER 1
+#endif
+#ifndef SM_ADV_GC
+#define SM_ADV_GC 2
 #endif
 
 typedef short v2i16 __attribute__((ext_vector_type(2)));
@@ -59,19 +65,28 @@ __device__ __forceinline__ uint32_t absdiff_u8x4(uint32_t a, uint32_t b) {
 template <int KF>
 __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                         int W, int H, int pitch, int64_t fstride, int D, int RB,
-                                                        int bands, int dsp, uint8_t* __restrict__ dif,
+                                                        int bands, int dsp, int gc, uint8_t* __restrict__ dif,
                                                         int64_t dstride) {
     constexpr int SEG = 16, NQ = 4;
     constexpr int kVPad = SEG;   // zero bytes in front of each staged R row (x - d down to -SEG)
     extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [RB][rstride]
-#if SM_ADV_ORDER
+#if SM_ADV_ORDER == 2
+    // gc chunks per group (gc divides dsp): id = (group, band-frame, chunk in group)
+    const int id = xcd_tile(blockIdx.x, gridDim.x);
+    const int nbf = (int)(gridDim.x / (unsigned)dsp);
+    const int cl = id % gc, rest = id / gc;
+    const int bf = rest % nbf, dz = (rest / nbf) * gc + cl;
+    const int f = bf / bands, y0 = (bf - f * bands) * RB;
+#elif SM_ADV_ORDER
     const int id = xcd_tile(blockIdx.x, gridDim.x);
     const int dz = id % dsp, bf = id / dsp;
     const int f = bf / bands, y0 = (bf - f * bands) * RB;
+    (void)gc;
 #else
     const int y0 = blockIdx.x * RB, f = blockIdx.y;
     const int dz = blockIdx.z;
     (void)bands;
+    (void)gc;
 #endif
     const int dc = (D + dsp - 1) / dsp;                           // disparities of this block
     const int d_begin = dz * dc, d_end = d_begin + dc < D ? d_begin + dc : D;
@@ -191,6 +206,7 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     // block x d chunks 1 x 2 (one row, 64 d per block) 52.3 us per frame; 4 x 16 48.0; 1 x 8 49.2;
     // 8 x 16 50.6; 4 x 32 59.6; plain instead of nontemporal stores 49.2
     const int dsplit = std::max(1, std::min(D, SM_ADV_MAXSPLIT));
+    const int gc = dsplit % SM_ADV_GC == 0 ? SM_ADV_GC : 1;
 #if SM_ADV_ORDER
     const int64_t nblk = (int64_t)bands * batch * dsplit;
     if (nblk > 0x7FFFFFFF) return hipErrorInvalidValue;
@@ -199,13 +215,13 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     const dim3 grid((unsigned)bands, (unsigned)batch, (unsigned)dsplit);
 #endif
     if (kf <= 1)
-        hipLaunchKernelGGL(ad_volume_kernel<1>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit,
+        hipLaunchKernelGGL(ad_volume_kernel<1>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
                            dif, dstride);
     else if (kf == 2)
-        hipLaunchKernelGGL(ad_volume_kernel<2>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit,
+        hipLaunchKernelGGL(ad_volume_kernel<2>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
                            dif, dstride);
     else
-        hipLaunchKernelGGL(ad_volume_kernel<4>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit,
+        hipLaunchKernelGGL(ad_volume_kernel<4>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
                            dif, dstride);
     return hipGetLastError();
 }

@@ -17,7 +17,15 @@ JOBS = (
     ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
     ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true", ["--agg", "guided", "--lr", "--batch", "32"],
      [1920, 1080, 128, 5, 32]),
+    # box + LR: the right-view matcher and its reduce, from the same runs
+    ("box_lr_r5_1080p_d128_b32", "box_match_kernel<5, 128, true", ["--agg", "box", "--lr", "--batch", "32"],
+     [1920, 1080, 128, 5, 32]),
+    ("box_lr_reduce_1080p_d128_b32", "right_reduce_lr_vec_kernel", ["--agg", "box", "--lr", "--batch", "32"],
+     [1920, 1080, 128, 5, 32]),
 )
+# SM_VALU_JOBS=name1,name2: only those jobs
+if os.environ.get("SM_VALU_JOBS"):
+    JOBS = tuple(j for j in JOBS if j[0] in os.environ["SM_VALU_JOBS"].split(","))
 
 
 # issue / wait breakdown of the guided kernels: wave cycles spent waiting at
@@ -44,7 +52,7 @@ def main():
             for row in csv.DictReader(open(f)):
                 if kname in row["Kernel_Name"]:
                     vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-        if "guided" in name:
+        if "guided" in name or "box_lr" in name:
             d2 = d + "_wait"
             cmd2 = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc"] + WAIT_CTRS.split() + [
                 "-d", d2, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
