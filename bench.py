@@ -263,53 +263,54 @@ def run_variants(sm, torch, dev, stream, seed):
         for (name, W, H, D, r) in (("host round trip 1080p 11x11 box d128", 1920, 1080, 128, 5),
                                    ("host round trip 463x370 9x9 box d64", 463, 370, 64, 4)):
             L, R = sm.synth_pair(seed, W, H, D)
-            for _ in range(3):
-                m.match(L, R, r, D)
             n = 20
-            t0 = time.perf_counter()
-            for _ in range(n):
-                m.match(L, R, r, D)
-            ms = (time.perf_counter() - t0) * 1000 / n
-            up, mt, dn = m.stage_ms()
+
+            def timed(call):
+                """ms per call of `call` with the handle at its default stage timing (auto, unarmed: no
+                stage-split events), then the (upload, match, download) split of a few recorded calls"""
+                m.set_stage_timing("auto")
+                for _ in range(3):
+                    call()
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    call()
+                ms = (time.perf_counter() - t0) * 1000 / n
+                m.stage_ms()                      # arms the recording for the calls below
+                for _ in range(3):
+                    call()
+                up, mt, dn = m.stage_ms()
+                m.set_stage_timing("auto")
+                return ms, {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}
+
+            ms, st = timed(lambda: m.match(L, R, r, D))
             out[name] = {"ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
-                         "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+                         "stage_ms": st}
             # the same call on caller frames / map in sm_host_alloc (page-locked) memory
             Lp, Rp, Op = sm.host_empty((H, W)), sm.host_empty((H, W)), sm.host_empty((H, W))
             Lp[...] = L
             Rp[...] = R
-            for _ in range(3):
-                m.match(Lp, Rp, r, D, out=Op)
-            t0 = time.perf_counter()
-            for _ in range(n):
-                m.match(Lp, Rp, r, D, out=Op)
-            ms = (time.perf_counter() - t0) * 1000 / n
-            up, mt, dn = m.stage_ms()
+            ms, st = timed(lambda: m.match(Lp, Rp, r, D, out=Op))
             out[name + " (sm_host_alloc buffers)"] = {
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
-                "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
+                "stage_ms": st}
             # the pair in one page-locked block (right frame after the left one): one upload copy
             pair = sm.host_empty((2, H, W))
             pair[0], pair[1] = L, R
-            for _ in range(3):
-                m.match(pair[0], pair[1], r, D, out=Op)
-            t0 = time.perf_counter()
-            for _ in range(n):
-                m.match(pair[0], pair[1], r, D, out=Op)
-            ms = (time.perf_counter() - t0) * 1000 / n
-            up, mt, dn = m.stage_ms()
+            ms, st = timed(lambda: m.match(pair[0], pair[1], r, D, out=Op))
             out[name + " (sm_host_alloc, pair in one block)"] = {
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
-                "stage_ms": {"upload": round(up, 4), "match": round(mt, 4), "download": round(dn, 4)}}
-            # the same without the stage-split events (SM_PARAM_STAGE_TIMING 0): the drop-in call's wall
-            m.set_stage_timing(False)
+                "stage_ms": st, "note": "timed at the default stage timing (no stage-split events); stage_ms "
+                "from 3 recorded calls after the timed ones"}
+            # the same with the stage-split events recorded in every call (SM_PARAM_STAGE_TIMING 1)
+            m.set_stage_timing(True)
             for _ in range(3):
                 m.match(pair[0], pair[1], r, D, out=Op)
             t0 = time.perf_counter()
             for _ in range(n):
                 m.match(pair[0], pair[1], r, D, out=Op)
             ms = (time.perf_counter() - t0) * 1000 / n
-            m.set_stage_timing(True)
-            out[name + " (sm_host_alloc, pair in one block, no stage timing)"] = {
+            m.set_stage_timing("auto")
+            out[name + " (sm_host_alloc, pair in one block, stage events in every call)"] = {
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1}
             del Lp, Rp, Op, pair
         # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's

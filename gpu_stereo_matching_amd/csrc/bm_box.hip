@@ -63,6 +63,11 @@ constexpr int kCols = 64;
 #define SM_RR_VEC 1
 #endif
 constexpr bool kRrVec = SM_RR_VEC != 0;
+// right-key rows skewed against bank conflicts of the scatter (Geo::RB_SKEW; SM_RB_SKEW=0: unskewed rows)
+#ifndef SM_RB_SKEW
+#define SM_RB_SKEW 1
+#endif
+constexpr bool kRbSkew = SM_RB_SKEW != 0;
 
 // pad slots in front of tile tx's partial row: lead + (u - tx*TW + dmax + 1) == 0 (mod 4) for u == 0 (mod 4)
 __host__ __device__ constexpr int rr_lead(int tx, int TW, int dmax) {
@@ -103,10 +108,23 @@ struct Geo {
     // entry of every u = 0 (mod 4) is 16-B aligned in every tile's row; pads are neutral (0xFFFFFFFF)
     static constexpr int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;
     static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
-    static constexpr int RB_BYTES = kTileH * RBW * 4;
+    // row j starts at rb_row(j) = j * RBW + skew(j & 15): a scatter's 32-lane group is rows hj = 0..15 of
+    // two quarter-rows 14 columns apart (NQ = 14), so the row starts must cover the banks = 0, 1 (mod 4)
+    // (their +14 the banks = 2, 3): skew 2 * (hj >> 1).  With RBW = 1 (mod 32) alone, rows 14, 15 of one
+    // quarter met rows 0, 1 of the next: every ds_min_u32 2-way conflicted (rocprof: 17 % of the kernel's
+    // LDS cycles were bank conflicts)
+    static constexpr int RB_SKEW = kRbSkew ? 2 : 0;
+    static constexpr int RB_BYTES = ((kTileH * RBW + 7 * RB_SKEW) * 4 + 15) & ~15;
     static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
     static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
+    __host__ __device__ static constexpr int rb_row(int j) { return j * RBW + RB_SKEW * ((j & 15) >> 1); }
 };
+
+// two right-view workgroups per CU at d_max 128 (8 waves) and 192 (6 waves), skewed rows included
+static_assert(Geo<1, 128, 8>::LDS_BYTES_R <= 81920 && Geo<5, 128, 8>::LDS_BYTES_R <= 81920 &&
+                  Geo<6, 128, 8>::LDS_BYTES_R <= 81920, "right view d_max 128: 2 workgroups per CU");
+static_assert(Geo<1, 192, 6>::LDS_BYTES_R <= 81920 && Geo<5, 192, 6>::LDS_BYTES_R <= 81920,
+              "right view d_max 192: 2 workgroups per CU (r = 6 needs 82.7 KB, one)");
 
 // 4 image bytes of row y from column x (little-endian), bytes outside the image read as 0.
 // Interior dwords are one (possibly unaligned) global_load_dword; border dwords go byte-wise.
@@ -258,7 +276,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     const int p_hi = ((wave + 1) * npairs) / NW;
     uint32_t* csw = cs + wave * (G::HALF * G::CSS);   // this wave's private half-tile CS plane
     if constexpr (RIGHT) {
-        for (int e = tid; e < kTileH * G::RBW; e += kThreads) rb[e] = 0xFFFFFFFFu;
+        for (int e = tid; e < G::RB_BYTES / 4; e += kThreads) rb[e] = 0xFFFFFFFFu;
     }
 
     __syncthreads();   // lq reads of the aliased staging area are done before any CS write
@@ -347,7 +365,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                 };
                 // RIGHT: klo of output o goes to u_o = x_o - d, khi to u_o - 1 = u_{o-1}; the two
                 // candidates of one u are min'ed in registers, one ds_min_u32 per u
-                uint32_t* rrow = rb + (h * G::HALF + hj) * G::RBW + (obase - d + DMAX + 1);   // + o: u_o
+                uint32_t* rrow = rb + G::rb_row(h * G::HALF + hj) + (obase - d + DMAX + 1);   // + o: u_o
                 uint32_t plo = 0xFFFFFFFFu;
                 if (!dm) {
 #pragma unroll
@@ -439,7 +457,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
         const int lead = rr_lead(tx, G::TW, DMAX);
         for (int e = tid; e < kTileH * G::PWP; e += kThreads) {
             const int j = e / G::PWP, k = e - j * G::PWP - lead;
-            P[e] = (k >= 0 && k < G::PW) ? rb[j * G::RBW + k] : 0xFFFFFFFFu;
+            P[e] = (k >= 0 && k < G::PW) ? rb[G::rb_row(j) + k] : 0xFFFFFFFFu;
         }
     }
 }

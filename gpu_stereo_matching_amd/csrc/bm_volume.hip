@@ -27,16 +27,17 @@ constexpr int kVT = 256;
 #ifndef SM_ADV_ROWS
 #define SM_ADV_ROWS 4      // image rows per block
 #endif
-// Block order (round 4).  1: one flat grid, the d chunk the fastest index and the ids
-// remapped XCD-contiguously (xcd_tile), so the dsplit blocks that stage the same band's L and R rows run
-// back to back on one XCD and fetch those rows from its L2 once.  0: the round-3 grid (band, frame,
-// chunk) in blockIdx (x, y, z), whose chunks of one band ran ~bands*frames blocks apart: each chunk
-// re-fetched the band from the fabric (rocprof FETCH: 1.17x the algorithmic bytes per launch).
-// 2: chunk groups — the dsplit chunks in groups of SM_ADV_GC, the group's chunks fastest and XCD-contiguous,
-// then the band, then the group: the band's rows are fetched dsplit / GC times (not dsplit), while the
-// blocks in flight write GC times the planes of order 0 (fewer, longer write streams than order 1).
+// Block order (round 4; profiles/microbench/r04_ad_order_ab.txt).  0 (default): the
+// grid (band, frame, chunk) in blockIdx (x, y, z): the blocks in flight write the 8 planes of one chunk
+// for ~8 frames, 64 long streams, but the chunks of one band run ~bands*frames blocks apart, so each
+// re-fetches the band from the fabric (rocprof FETCH 1.17x the algorithmic bytes at 16 chunks).
+// 1: one flat grid, the d chunk the fastest index and the ids remapped XCD-contiguously (xcd_tile): the
+// band is fetched once (1.0001x), but the blocks in flight write all D planes at once and the launch
+// runs 63 us per 1080p frame against 48 (HIP events, same box).
+// 2: chunk groups of SM_ADV_GC, the group's chunks fastest and XCD-contiguous, then the band, then the
+// group (GC 1 / 2 / 4: 54 / 59 / 59 us).  3: (band, chunk, frame), a band's chunks `bands` blocks apart.
 #ifndef SM_ADV_ORDER
-#define SM_ADV_ORDER 1
+#define SM_ADV_ORDER 0
 #endif
 #ifndef SM_ADV_GC
 #define SM_ADV_GC 2
@@ -77,6 +78,11 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     const int cl = id % gc, rest = id / gc;
     const int bf = rest % nbf, dz = (rest / nbf) * gc + cl;
     const int f = bf / bands, y0 = (bf - f * bands) * RB;
+#elif SM_ADV_ORDER == 3
+    // (band, chunk, frame): a band's chunks run `bands` blocks apart instead of bands * frames
+    const int y0 = blockIdx.x * RB, dz = blockIdx.y, f = blockIdx.z;
+    (void)bands;
+    (void)gc;
 #elif SM_ADV_ORDER
     const int id = xcd_tile(blockIdx.x, gridDim.x);
     const int dz = id % dsp, bf = id / dsp;
@@ -207,7 +213,9 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     // 8 x 16 50.6; 4 x 32 59.6; plain instead of nontemporal stores 49.2
     const int dsplit = std::max(1, std::min(D, SM_ADV_MAXSPLIT));
     const int gc = dsplit % SM_ADV_GC == 0 ? SM_ADV_GC : 1;
-#if SM_ADV_ORDER
+#if SM_ADV_ORDER == 3
+    const dim3 grid((unsigned)bands, (unsigned)dsplit, (unsigned)batch);
+#elif SM_ADV_ORDER
     const int64_t nblk = (int64_t)bands * batch * dsplit;
     if (nblk > 0x7FFFFFFF) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblk);

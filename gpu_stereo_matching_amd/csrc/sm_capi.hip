@@ -988,6 +988,7 @@ SM_API int sm_set_param_f(sm_handle* h, int param, float value) {
     if (param == SM_PARAM_STAGE_TIMING) {
         if (value != 0.f && value != 1.f && value != 2.f) return fail(SM_ERR_INVALID_ARG, "stage timing is 0, 1 or 2");
         h->stage_timing = (int)value;
+        if (h->stage_timing == 2) h->stage_requested = false;   // back to the default: unarmed until read
         return SM_OK;
     }
 

@@ -72,7 +72,8 @@ enum {
                                   compute queues, ~10 us per 1080p call together).  2 (default, auto):
                                   recorded once sm_last_stage_ms has been called on the handle (the calls
                                   after that first read), or in every call when the environment sets
-                                  SM_VERBOSE; 1: always; 0: never, and sm_last_stage_ms reports 0 */
+                                  SM_VERBOSE; 1: always; 0: never, and sm_last_stage_ms reports 0.
+                                  Setting 2 again returns to the unarmed default */
 };
 
 typedef struct sm_handle sm_handle;

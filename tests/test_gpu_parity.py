@@ -401,8 +401,10 @@ def test_stage_timings(sm, gray, oracle):
         m.set_stage_timing(True)
         m.match(L, R, 5, 64)
         assert min(m.stage_ms()) > 0
-        m.set_stage_timing("auto")                   # already armed on this handle
+        m.set_stage_timing("auto")                   # back to the default: unarmed again
         m.match(L, R, 5, 64)
+        assert m.stage_ms() == (0.0, 0.0, 0.0)
+        m.match(L, R, 5, 64)                         # armed by that read
         assert min(m.stage_ms()) > 0
     assert np.array_equal(want, oracle.box_disp(L, R, 5, 64))
 
