@@ -108,16 +108,21 @@ struct Geo {
     // entry of every u = 0 (mod 4) is 16-B aligned in every tile's row; pads are neutral (0xFFFFFFFF)
     static constexpr int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;
     static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
-    // row j starts at rb_row(j) = j * RBW + skew(j & 15): a scatter's 32-lane group is rows hj = 0..15 of
-    // two quarter-rows 14 columns apart (NQ = 14), so the row starts must cover the banks = 0, 1 (mod 4)
-    // (their +14 the banks = 2, 3): skew 2 * (hj >> 1).  With RBW = 1 (mod 32) alone, rows 14, 15 of one
-    // quarter met rows 0, 1 of the next: every ds_min_u32 2-way conflicted (rocprof: 17 % of the kernel's
-    // LDS cycles were bank conflicts)
+    // row j starts at rb_row(j) = j * RBW + skew(j): a scatter's 32-lane group is rows hj = 0..15 of two
+    // quarter-rows 14 columns apart (NQ = 14), so the row starts must cover the banks = 0, 1 (mod 4)
+    // (their +14 the banks = 2, 3): skew 2 * (hj >> 1), plus 16 for the second 16-row half so that the
+    // skew never decreases from one row to the next (a row keeps its full RBW entries; rows 15 and 16
+    // overlapped by 4 entries when the skew restarted at 0).  With RBW = 1 (mod 32) alone, rows 14, 15 of
+    // one quarter met rows 0, 1 of the next: every ds_min_u32 2-way conflicted (rocprof: 17 % of the
+    // kernel's LDS cycles were bank conflicts; 1.5 % with the skew)
     static constexpr int RB_SKEW = kRbSkew ? 2 : 0;
-    static constexpr int RB_BYTES = ((kTileH * RBW + 7 * RB_SKEW) * 4 + 15) & ~15;
+    static constexpr int RB_BYTES = ((kTileH * RBW + 15 * RB_SKEW) * 4 + 15) & ~15;
     static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
     static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
-    __host__ __device__ static constexpr int rb_row(int j) { return j * RBW + RB_SKEW * ((j & 15) >> 1); }
+    __host__ __device__ static constexpr int rb_row(int j) {
+        return j * RBW + RB_SKEW * (((j & 15) >> 1) + 8 * (j >> 4));
+    }
+    static_assert(kTileH == 32, "rb_row's skew covers two 16-row halves");
 };
 
 // two right-view workgroups per CU at d_max 128 (8 waves) and 192 (6 waves), skewed rows included

@@ -18,14 +18,18 @@ namespace sm {
 namespace {
 
 constexpr int kVT = 256;
+// Round 4 (profiles/microbench/r04_ad_order_ab.txt): 2 d chunks of 2-row bands.  Each
+// chunk re-reads its band, so the fabric traffic is ~(1 + chunks * 2 / (D + 2)) x the algorithmic bytes:
+// rocprof 1.013x at 2 chunks (0.408 ms per 8-frame launch, 0.661 of 8 TB/s), against 1.166x at the round-3
+// 16 chunks of 4 rows (0.40-0.44 ms) and 1.083x at 8 (0.400 ms).
 #ifndef SM_ADV_MAXSPLIT
-#define SM_ADV_MAXSPLIT 16   // d chunks per (band, frame): 8 d per block at D = 128
+#define SM_ADV_MAXSPLIT 2    // d chunks per (band, frame): 64 d per block at D = 128
 #endif
 #ifndef SM_ADV_NT
 #define SM_ADV_NT 1
 #endif
 #ifndef SM_ADV_ROWS
-#define SM_ADV_ROWS 4      // image rows per block
+#define SM_ADV_ROWS 2      // image rows per block
 #endif
 // Block order (round 4; profiles/microbench/r04_ad_order_ab.txt).  0 (default): the
 // grid (band, frame, chunk) in blockIdx (x, y, z): the blocks in flight write the 8 planes of one chunk
@@ -208,9 +212,10 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     const int kf = (rb * nseg + kVT - 1) / kVT;
     const size_t lds = (size_t)rb * ((SEG + nseg * SEG + 4) / 4) * 4;
     const int bands = (H + rb - 1) / rb;
-    // Same-box A/B, 8 x 1080p D = 128 frames per launch (tools/ab_staged_kernels.py, 5 rounds): rows per
-    // block x d chunks 1 x 2 (one row, 64 d per block) 52.3 us per frame; 4 x 16 48.0; 1 x 8 49.2;
-    // 8 x 16 50.6; 4 x 32 59.6; plain instead of nontemporal stores 49.2
+    // Same-box A/B, 8 x 1080p D = 128 frames per launch (tools/ab_staged_kernels.py, HIP events), rows per
+    // block x d chunks, round 3: 1 x 2 52.3 us per frame; 4 x 16 48.0; 1 x 8 49.2; 8 x 16 50.6; 4 x 32
+    // 59.6; plain instead of nontemporal stores 49.2.  Round 4 (one box): 4 x 16 50.2; 4 x 8 50.7;
+    // 2 x 4 50.7; 4 x 2 53.7; 2 x 2 52.1 (kept: the fewest re-reads of the band, see SM_ADV_MAXSPLIT)
     const int dsplit = std::max(1, std::min(D, SM_ADV_MAXSPLIT));
     const int gc = dsplit % SM_ADV_GC == 0 ? SM_ADV_GC : 1;
 #if SM_ADV_ORDER == 3
