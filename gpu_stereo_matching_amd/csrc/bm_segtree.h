@@ -18,8 +18,16 @@ struct StWorkspace {
     int* task = nullptr;       // per tree: the wave filter's level tasks (int4 each), up to 2 * (P + levels)
     uint32_t* sortbuf = nullptr;   // edge sort: keys and values (2 x 2 nE), digit counts, sorted edges (3 nE)
     void* h_edges[2] = {nullptr, nullptr};   // page-locked host copies of sorted edges (12 B each), 2 trees
+    // page-locked host trees (round 4), one per tree slot: ints in the device slot's layout (rank, parent,
+    // first, child: 4P; level offsets: P + 2), then pdist (P bytes): one DMA copy per tree
+    void* h_tree[2] = {nullptr, nullptr};
+    // the sorted edges come down in kEdgeChunks copies, each followed by its event (the host tree starts
+    // on the first chunk)
+    static constexpr int kEdgeChunks = 4;
+    hipEvent_t edge_ev[2][kEdgeChunks] = {};
+    int edge_chunk[2] = {0, 0};   // edges per chunk of each slot's last download
     size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0, sortbuf_n = 0;
-    size_t h_edges_n[2] = {0, 0};
+    size_t h_edges_n[2] = {0, 0}, h_tree_n[2] = {0, 0};
     ~StWorkspace();
     void release();
 };

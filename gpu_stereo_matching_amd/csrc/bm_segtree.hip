@@ -639,7 +639,33 @@ hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* w
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     nE = n;
-    return hipMemcpyAsync(ws.h_edges[slot], edges, hbytes, hipMemcpyDeviceToHost, s);
+    // down in kEdgeChunks copies, each followed by its event: the host tree's first pass starts on the
+    // first chunk (wait_edges) while the rest is still in flight
+    constexpr int K = StWorkspace::kEdgeChunks;
+    const int chunk = (n + K - 1) / K;
+    ws.edge_chunk[slot] = chunk;
+    for (int k = 0; k < K; ++k) {
+        if (!ws.edge_ev[slot][k] &&
+            (e = hipEventCreateWithFlags(&ws.edge_ev[slot][k], hipEventDisableTiming)) != hipSuccess)
+            return e;
+        const int lo = std::min(n, k * chunk), hi = std::min(n, lo + chunk);
+        if (hi > lo && (e = hipMemcpyAsync(static_cast<st_host::Edge*>(ws.h_edges[slot]) + lo, edges + lo,
+                                           (size_t)(hi - lo) * sizeof(st_host::Edge), hipMemcpyDeviceToHost, s)) !=
+                           hipSuccess)
+            return e;
+        if ((e = hipEventRecord(ws.edge_ev[slot][k], s)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// Blocks until the sorted edges [0, upto) of `slot` have landed on the host (the chunk events of
+// gpu_sorted_edges); false if an event reports an error.
+bool wait_edges(StWorkspace& ws, int slot, int upto) {
+    const int chunk = std::max(ws.edge_chunk[slot], 1);
+    const int last = std::min(StWorkspace::kEdgeChunks, (upto + chunk - 1) / chunk);
+    for (int k = 0; k < last; ++k)
+        if (hipEventSynchronize(ws.edge_ev[slot][k]) != hipSuccess) return false;
+    return true;
 }
 
 // One tree on the device: workspace slot k holds int [rank | parent | first | child | lev] (5P + 2),
@@ -673,17 +699,35 @@ void weight_table(float sigma, float* table) {
     for (int i = 0; i <= 255; ++i) table[i] = std::exp(-float(i) / (255 * sg));
 }
 
-// `t` and `table` must stay alive until the stream has consumed the copies
+// Page-locked host tree of slot k (StWorkspace::h_tree): ints (5P + 2) in the device slot's layout, then
+// pdist (P bytes); the slot's previous upload must have completed before a new tree is bound to it.
+hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree& t) {
+    const size_t need = (size_t)(5 * P + 2) * 4 + (size_t)P;
+    if (ws.h_tree_n[k] < need) {
+        if (ws.h_tree[k]) (void)hipHostFree(ws.h_tree[k]);
+        ws.h_tree[k] = nullptr;
+        ws.h_tree_n[k] = 0;
+        const hipError_t e = hipHostMalloc(&ws.h_tree[k], need, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        ws.h_tree_n[k] = need;
+    }
+    int* ints = static_cast<int*>(ws.h_tree[k]);
+    t.bind((int)P, ints, reinterpret_cast<uint8_t*>(ints + 5 * P + 2));
+    return hipSuccess;
+}
+
+// A tree bound by host_tree_slot: its level offsets join the ints, which go up as one copy (rank .. lev),
+// then pdist and the weight table.  `t`'s slot and `table` must stay alive until the stream has consumed
+// the copies.
 hipError_t upload_tree(const HostTree& t, const float* table, int64_t P, DevTree& d, hipStream_t s) {
     d.nlev = (int)t.lev.size() - 1;
     if ((size_t)d.nlev + 1 > (size_t)P + 2) return hipErrorInvalidValue;
+    int* ints = t.rank;
+    std::copy(t.lev.begin(), t.lev.end(), ints + 4 * P);
     hipError_t e;
-    if ((e = hipMemcpyAsync(d.rank, t.rank.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(d.parent, t.parent.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(d.first, t.first.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(d.child, t.child.data(), (size_t)P * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(d.lev, t.lev.data(), t.lev.size() * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(d.pdist, t.pdist.data(), (size_t)P, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d.rank, ints, ((size_t)4 * P + t.lev.size()) * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+    if ((e = hipMemcpyAsync(d.pdist, t.pdist, (size_t)P, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     return hipMemcpyAsync(d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s);
 }
 
@@ -778,6 +822,13 @@ void StWorkspace::release() {
         if (h_edges[k]) (void)hipHostFree(h_edges[k]);
         h_edges[k] = nullptr;
         h_edges_n[k] = 0;
+        if (h_tree[k]) (void)hipHostFree(h_tree[k]);
+        h_tree[k] = nullptr;
+        h_tree_n[k] = 0;
+        for (auto& ev : edge_ev[k]) {
+            if (ev) (void)hipEventDestroy(ev);
+            ev = nullptr;
+        }
     }
     w8 = nullptr;
     grad = nullptr;
@@ -818,11 +869,16 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
     ST_CHK(hipGetLastError());
-    ST_CHK(hipStreamSynchronize(s));
-    // tree on the host
+    // tree on the host, into page-locked memory, starting on the first edge chunk (no stream sync: the
+    // gradients run meanwhile)
     const auto t0 = std::chrono::steady_clock::now();
     HostTree t;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t)) return hipErrorInvalidValue;
+    ST_CHK(host_tree_slot(ws, P, 0, t));
+    bool arrived = true;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t, ws.edge_chunk[0],
+                         [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
+        !arrived)
+        return hipErrorInvalidValue;
     float table[256];
     weight_table(sigma, table);
     const float tree_ms = ms_since(t0);
@@ -889,26 +945,28 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
     ST_CHK(hipGetLastError());
-    ST_CHK(hipStreamSynchronize(s));
     // first run: colour trees of the left and the right view, built side by side (StereoDisparity.cpp:112-123)
+    // into page-locked slots 0 and 1, each starting on the first chunk of its edges
     auto t0 = std::chrono::steady_clock::now();
     HostTree tl, tr;
-    bool okR = false;
+    ST_CHK(host_tree_slot(ws, P, 0, tl));
+    ST_CHK(host_tree_slot(ws, P, 1, tr));
     // neither build may leave its exception behind the other's thread (a joinable std::thread must not
     // be destroyed): a failed build reports false
-    std::thread th([&] {
+    auto build = [&](int slot, HostTree& t) {
         try {
-            okR = tree_from_edges(static_cast<Edge*>(ws.h_edges[1]), nE, (int)P, W, tau, 1.0f, tr);
+            bool arrived = true;
+            const bool ok = tree_from_edges(static_cast<Edge*>(ws.h_edges[slot]), nE, (int)P, W, tau, 1.0f, t,
+                                            ws.edge_chunk[slot],
+                                            [&](int upto) { arrived = arrived && wait_edges(ws, slot, upto); });
+            return ok && arrived;
         } catch (...) {
-            okR = false;
+            return false;
         }
-    });
-    bool okL = false;
-    try {
-        okL = tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, tl);
-    } catch (...) {
-        okL = false;
-    }
+    };
+    bool okR = false;
+    std::thread th([&] { okR = build(1, tr); });
+    const bool okL = build(0, tl);
     th.join();
     if (!okL || !okR) return hipErrorInvalidValue;
     float tab1[256];
@@ -948,10 +1006,17 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // re-segmentation: colour + depth tree on the left view (StereoDisparity.cpp:150-152), its weights
     // from the first left map and mask, sorted on the GPU
     ST_CHK(gpu_sorted_edges(ws, wrL, wrL + P, mapL, mask, (float)D, W, H, true, 0, s, nE));
-    ST_CHK(hipStreamSynchronize(s));
+    // the first run's uploads from page-locked slot 0 were enqueued before this download: once its first
+    // chunk has landed, slot 0 is free for the depth tree
+    if (!wait_edges(ws, 0, 1)) return hipErrorUnknown;
     t0 = std::chrono::steady_clock::now();
     HostTree td;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td)) return hipErrorInvalidValue;
+    ST_CHK(host_tree_slot(ws, P, 0, td));
+    bool arrived = true;
+    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td, ws.edge_chunk[0],
+                         [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
+        !arrived)
+        return hipErrorInvalidValue;
     float tab2[256];
     weight_table(sigma, tab2);
     tree_ms += ms_since(t0);

@@ -20,10 +20,34 @@ namespace sm {
 namespace st_host {
 
 // ---- host: the tree (sequential, as the reference's) ----
+// rank | parent | first | child (P ints each) sit in one block laid out as the device's tree slot (round 4),
+// in the tree's own vector or, after bind(), in caller storage (the GPU path binds page-locked memory, so
+// the tree goes up as one DMA copy without a staging memcpy); pdist likewise.  node and lev stay vectors.
 struct HostTree {
-    std::vector<int> node, rank, parent, first, lev;
-    std::vector<uint8_t> pdist;
-    std::vector<uint32_t> child;
+    std::vector<int> node, lev;
+    int* rank = nullptr;
+    int* parent = nullptr;
+    int* first = nullptr;
+    uint32_t* child = nullptr;
+    uint8_t* pdist = nullptr;
+    std::vector<int> own_i;
+    std::vector<uint8_t> own_b;
+    // ints: 4P (+ the caller's room after them); bytes: P.  Null storage: the tree's own vectors.
+    void bind(int P, int* ints = nullptr, uint8_t* bytes = nullptr) {
+        if (!ints) {
+            own_i.resize((size_t)4 * P);
+            ints = own_i.data();
+        }
+        if (!bytes) {
+            own_b.resize((size_t)P);
+            bytes = own_b.data();
+        }
+        rank = ints;
+        parent = ints + P;
+        first = ints + 2 * (size_t)P;
+        child = reinterpret_cast<uint32_t*>(ints + 3 * (size_t)P);
+        pdist = bytes;
+    }
 };
 
 struct Edge {
@@ -86,7 +110,12 @@ std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P)
 // first one joined (their ends already share a root) and appends each marked edge to the neighbour
 // lists as it goes, which is the sorted-edge order of SegmentTree.cpp:74-95 without a third pass; the
 // lists are 8 B per pixel (four distances, four 2-bit directions, the count) instead of 24.
-bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
+// `arrived(i)` (round 4) returns once edges [0, i) are readable: the GPU path downloads the sorted edges in
+// chunks and the first pass starts on the first chunk while the rest is still in flight.  It is called
+// with increasing i at most every `step` edges, and with nE before the second pass.  The tree's arrays
+// must be bound (HostTree::bind) unless it owns none yet.
+template <class Arrived>
+bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step, Arrived&& arrived) {
 SM_ST_NO_CONTRACT
     // segment_graph (segment-graph.h:48-101) on disjoint-set.h's forest (Dsu's rules, roots packed)
     std::vector<int> par(P);
@@ -115,7 +144,12 @@ SM_ST_NO_CONTRACT
         return y;
     };
     std::vector<uint8_t> mask(nE, 0);
+    int avail = 0;
     for (int i = 0; i < nE; ++i) {
+        if (i == avail) {
+            avail = std::min(nE, avail + std::max(step, 1));
+            arrived(avail);
+        }
         const int a = find(e[i].a), b = find(e[i].b);
         if (a != b && e[i].w <= R[a].thr && e[i].w <= R[b].thr) {
             mask[i] = 1;
@@ -152,15 +186,15 @@ SM_ST_NO_CONTRACT
         const float sw = e[i].w * wscale;
         link(e[i].a, e[i].b, (uint8_t)std::min((int)(sw + 0.5f), 255));
     }
-    // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level
+    // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level; every entry is written once the tree
+    // spans the image (end == P), so the arrays need no clearing beyond the root's
     const int off[4] = {-1, 1, -W, W};
-    t.node.assign(P, 0);
-    t.rank.assign(P, 0);
-    t.parent.assign(P, -1);
-    t.first.assign(P, 0);
-    t.pdist.assign(P, 0);
-    t.child.assign(P, 0);
+    if (!t.rank) t.bind(P);
+    t.node.resize(P);
     t.lev.assign(1, 0);
+    t.node[0] = 0;
+    t.parent[0] = -1;
+    t.pdist[0] = 0;
     // the marked edges form a forest, so a node's neighbours other than its parent are exactly the ones
     // BFS has not visited yet (SegmentTree.cpp:116's visited test): compare with the parent's pixel
     std::vector<int> ppix(P);
@@ -190,6 +224,11 @@ SM_ST_NO_CONTRACT
         }
     }
     return end == P;
+}
+
+// every edge already in memory
+bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
+    return tree_from_edges(e, nE, P, W, tau, wscale, t, nE, [](int) {});
 }
 
 bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {

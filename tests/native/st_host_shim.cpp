@@ -9,8 +9,8 @@ using namespace sm::st_host;
 
 static int export_tree(const HostTree& t, int P, int* node, int* parent, uint8_t* pdist) {
     std::memcpy(node, t.node.data(), sizeof(int) * P);
-    std::memcpy(parent, t.parent.data(), sizeof(int) * P);
-    std::memcpy(pdist, t.pdist.data(), (size_t)P);
+    std::memcpy(parent, t.parent, sizeof(int) * P);
+    std::memcpy(pdist, t.pdist, (size_t)P);
     return (int)t.lev.size() - 1;
 }
 
