@@ -21,6 +21,7 @@ struct StWorkspace {
     // page-locked host trees (round 4), one per tree slot: ints in the device slot's layout (rank, parent,
     // first, child: 4P; level offsets: P + 2), then pdist (P bytes): one DMA copy per tree
     void* h_tree[2] = {nullptr, nullptr};
+    void* host_tree[2] = {nullptr, nullptr};   // st_host::HostTree per slot, reused across calls (bm_segtree.hip)
     // the sorted edges come down in kEdgeChunks copies, each followed by its event (the host tree starts
     // on the first chunk)
     static constexpr int kEdgeChunks = 4;

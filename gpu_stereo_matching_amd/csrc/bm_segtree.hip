@@ -701,7 +701,10 @@ void weight_table(float sigma, float* table) {
 
 // Page-locked host tree of slot k (StWorkspace::h_tree): ints (5P + 2) in the device slot's layout, then
 // pdist (P bytes); the slot's previous upload must have completed before a new tree is bound to it.
-hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree& t) {
+hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree*& tp) {
+    if (!ws.host_tree[k]) ws.host_tree[k] = new HostTree();
+    tp = static_cast<HostTree*>(ws.host_tree[k]);
+    HostTree& t = *tp;
     const size_t need = (size_t)(5 * P + 2) * 4 + (size_t)P;
     if (ws.h_tree_n[k] < need) {
         if (ws.h_tree[k]) (void)hipHostFree(ws.h_tree[k]);
@@ -825,6 +828,8 @@ void StWorkspace::release() {
         if (h_tree[k]) (void)hipHostFree(h_tree[k]);
         h_tree[k] = nullptr;
         h_tree_n[k] = 0;
+        delete static_cast<st_host::HostTree*>(host_tree[k]);
+        host_tree[k] = nullptr;
         for (auto& ev : edge_ev[k]) {
             if (ev) (void)hipEventDestroy(ev);
             ev = nullptr;
@@ -872,8 +877,9 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     // tree on the host, into page-locked memory, starting on the first edge chunk (no stream sync: the
     // gradients run meanwhile)
     const auto t0 = std::chrono::steady_clock::now();
-    HostTree t;
-    ST_CHK(host_tree_slot(ws, P, 0, t));
+    HostTree* tp = nullptr;
+    ST_CHK(host_tree_slot(ws, P, 0, tp));
+    HostTree& t = *tp;
     bool arrived = true;
     if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t, ws.edge_chunk[0],
                          [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
@@ -948,9 +954,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // first run: colour trees of the left and the right view, built side by side (StereoDisparity.cpp:112-123)
     // into page-locked slots 0 and 1, each starting on the first chunk of its edges
     auto t0 = std::chrono::steady_clock::now();
-    HostTree tl, tr;
-    ST_CHK(host_tree_slot(ws, P, 0, tl));
-    ST_CHK(host_tree_slot(ws, P, 1, tr));
+    HostTree *tlp = nullptr, *trp = nullptr;
+    ST_CHK(host_tree_slot(ws, P, 0, tlp));
+    ST_CHK(host_tree_slot(ws, P, 1, trp));
+    HostTree &tl = *tlp, &tr = *trp;
     // neither build may leave its exception behind the other's thread (a joinable std::thread must not
     // be destroyed): a failed build reports false
     auto build = [&](int slot, HostTree& t) {
@@ -1010,8 +1017,9 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // chunk has landed, slot 0 is free for the depth tree
     if (!wait_edges(ws, 0, 1)) return hipErrorUnknown;
     t0 = std::chrono::steady_clock::now();
-    HostTree td;
-    ST_CHK(host_tree_slot(ws, P, 0, td));
+    HostTree* tdp = nullptr;   // slot 0's tree object again: the left tree's tasks are uploaded
+    ST_CHK(host_tree_slot(ws, P, 0, tdp));
+    HostTree& td = *tdp;
     bool arrived = true;
     if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td, ws.edge_chunk[0],
                          [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||

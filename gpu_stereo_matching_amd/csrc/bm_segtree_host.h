@@ -9,6 +9,11 @@
 #include <cstdlib>
 #include <vector>
 
+// phase marks for tools/microbench/st_host_bench.cpp (0: first pass, 1: second pass + lists, 2: BFS done)
+#ifndef SM_ST_PHASE
+#define SM_ST_PHASE(k)
+#endif
+
 // the float steps (thresholds, tree distances, depth weights) are rounded one operation at a time
 #if defined(__clang__)
 #define SM_ST_NO_CONTRACT _Pragma("clang fp contract(off)")
@@ -23,8 +28,25 @@ namespace st_host {
 // rank | parent | first | child (P ints each) sit in one block laid out as the device's tree slot (round 4),
 // in the tree's own vector or, after bind(), in caller storage (the GPU path binds page-locked memory, so
 // the tree goes up as one DMA copy without a staging memcpy); pdist likewise.  node and lev stay vectors.
+// a root's threshold (segment-graph.h:63, tau / 1 at the start), size and rank in one record
+struct RootRec {
+    float thr;
+    int size, rank;
+};
+// neighbour list of a pixel: direction k is (dir >> 2k) & 3 -> offset -1, +1, -W, +W, distance byte k of d
+struct AdjRec {
+    uint32_t d;
+    uint16_t dir, n;
+};
+
 struct HostTree {
     std::vector<int> node, lev;
+    // the builder's scratch (round 4): kept with the tree, so a tree object reused from call to call (the
+    // GPU path keeps one per slot) touches memory that is already mapped instead of ~5 MB of fresh pages
+    std::vector<int> par, ppix;
+    std::vector<RootRec> roots;
+    std::vector<AdjRec> adj;
+    std::vector<uint8_t> mask;
     int* rank = nullptr;
     int* parent = nullptr;
     int* first = nullptr;
@@ -118,13 +140,11 @@ template <class Arrived>
 bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step, Arrived&& arrived) {
 SM_ST_NO_CONTRACT
     // segment_graph (segment-graph.h:48-101) on disjoint-set.h's forest (Dsu's rules, roots packed)
-    std::vector<int> par(P);
+    std::vector<int>& par = t.par;
+    par.resize(P);
     for (int i = 0; i < P; ++i) par[i] = i;
-    struct Root {
-        float thr;   // segment-graph.h:63 threshold, tau / 1 at the start
-        int size, rank;
-    };
-    std::vector<Root> R(P, Root{tau / 1, 1, 0});
+    std::vector<RootRec>& R = t.roots;
+    R.assign(P, RootRec{tau / 1, 1, 0});
     auto find = [&](int x) {   // path halving, as Dsu::find
         while (x != par[x]) {
             par[x] = par[par[x]];
@@ -143,7 +163,8 @@ SM_ST_NO_CONTRACT
         if (R[x].rank == R[y].rank) R[y].rank++;
         return y;
     };
-    std::vector<uint8_t> mask(nE, 0);
+    std::vector<uint8_t>& mask = t.mask;
+    mask.assign(nE, 0);
     int avail = 0;
     for (int i = 0; i < nE; ++i) {
         if (i == avail) {
@@ -157,20 +178,18 @@ SM_ST_NO_CONTRACT
             R[r].thr = e[i].w + tau / R[r].size;
         }
     }
-    // neighbour lists: direction k of pixel p is (dir >> 2k) & 3 -> offset -1, +1, -W, +W
-    struct Adj {
-        uint32_t d;
-        uint16_t dir, n;
-    };
-    std::vector<Adj> adj(P, Adj{0u, 0, 0});
+    SM_ST_PHASE(0);
+    // neighbour lists (AdjRec)
+    std::vector<AdjRec>& adj = t.adj;
+    adj.assign(P, AdjRec{0u, 0, 0});
     auto link = [&](int pa, int pb, uint8_t dis) {
         const int diff = pb - pa;
         const uint32_t da = diff == -1 ? 0u : diff == 1 ? 1u : diff < 0 ? 2u : 3u;
-        Adj& A = adj[pa];
+        AdjRec& A = adj[pa];
         A.d |= (uint32_t)dis << (8 * A.n);
         A.dir |= (uint16_t)(da << (2 * A.n));
         A.n++;
-        Adj& B = adj[pb];
+        AdjRec& B = adj[pb];
         B.d |= (uint32_t)dis << (8 * B.n);
         B.dir |= (uint16_t)((da ^ 1u) << (2 * B.n));
         B.n++;
@@ -186,6 +205,7 @@ SM_ST_NO_CONTRACT
         const float sw = e[i].w * wscale;
         link(e[i].a, e[i].b, (uint8_t)std::min((int)(sw + 0.5f), 255));
     }
+    SM_ST_PHASE(1);
     // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level; every entry is written once the tree
     // spans the image (end == P), so the arrays need no clearing beyond the root's
     const int off[4] = {-1, 1, -W, W};
@@ -197,7 +217,8 @@ SM_ST_NO_CONTRACT
     t.pdist[0] = 0;
     // the marked edges form a forest, so a node's neighbours other than its parent are exactly the ones
     // BFS has not visited yet (SegmentTree.cpp:116's visited test): compare with the parent's pixel
-    std::vector<int> ppix(P);
+    std::vector<int>& ppix = t.ppix;
+    ppix.resize(P);
     ppix[0] = -1;
     int end = 1;
     for (int lo = 0, hi = 1; lo < hi; lo = hi, hi = end) {
@@ -207,7 +228,7 @@ SM_ST_NO_CONTRACT
             t.rank[p] = i;
             t.first[i] = end;
             uint32_t ch = 0, n = 0;
-            const Adj A = adj[p];
+            const AdjRec A = adj[p];
             for (int k = 0; k < A.n; ++k) {
                 const int q = p + off[(A.dir >> (2 * k)) & 3];
                 if (q == pp) continue;
@@ -223,6 +244,7 @@ SM_ST_NO_CONTRACT
             t.child[i] = ch | n;
         }
     }
+    SM_ST_PHASE(2);
     return end == P;
 }
 
