@@ -224,6 +224,13 @@ SM_ST_NO_CONTRACT
     for (int lo = 0, hi = 1; lo < hi; lo = hi, hi = end) {
         t.lev.push_back(hi);
         for (int i = lo; i < hi; ++i) {
+            // the neighbour list and rank slot of the node 8 places on (already queued: BFS order):
+            // BFS 1.58 -> 1.45 ms on the GPU box's host for Art (profiles/microbench/r04_st_host_phases.txt;
+            // the same prefetch in the two edge passes made them slower)
+            if (i + 8 < end) {
+                __builtin_prefetch(&adj[t.node[i + 8]]);
+                __builtin_prefetch(&t.rank[t.node[i + 8]]);
+            }
             const int p = t.node[i], pp = ppix[i];
             t.rank[p] = i;
             t.first[i] = end;
