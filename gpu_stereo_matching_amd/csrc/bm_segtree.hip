@@ -883,8 +883,10 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     bool arrived = true;
     if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t, ws.edge_chunk[0],
                          [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
-        !arrived)
+        !arrived) {
+        (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
+    }
     float table[256];
     weight_table(sigma, table);
     const float tree_ms = ms_since(t0);
@@ -975,7 +977,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     std::thread th([&] { okR = build(1, tr); });
     const bool okL = build(0, tl);
     th.join();
-    if (!okL || !okR) return hipErrorInvalidValue;
+    if (!okL || !okR) {
+        (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
+        return hipErrorInvalidValue;
+    }
     float tab1[256];
     weight_table(kSigmaOne, tab1);
     float tree_ms = ms_since(t0);
@@ -1015,7 +1020,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(gpu_sorted_edges(ws, wrL, wrL + P, mapL, mask, (float)D, W, H, true, 0, s, nE));
     // the first run's uploads from page-locked slot 0 were enqueued before this download: once its first
     // chunk has landed, slot 0 is free for the depth tree
-    if (!wait_edges(ws, 0, 1)) return hipErrorUnknown;
+    if (!wait_edges(ws, 0, 1)) {
+        (void)hipStreamSynchronize(s);
+        return hipErrorUnknown;
+    }
     t0 = std::chrono::steady_clock::now();
     HostTree* tdp = nullptr;   // slot 0's tree object again: the left tree's tasks are uploaded
     ST_CHK(host_tree_slot(ws, P, 0, tdp));
@@ -1023,8 +1031,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     bool arrived = true;
     if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td, ws.edge_chunk[0],
                          [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
-        !arrived)
+        !arrived) {
+        (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
+    }
     float tab2[256];
     weight_table(sigma, tab2);
     tree_ms += ms_since(t0);
