@@ -99,18 +99,22 @@ constexpr bool kGuidedRoles = SM_G_ROLES != 0;
 // frame): guided 453.3 (32-row tiles) -> 851.0 (tall), guided + LR 524.7 -> 953.2 with the right view
 // tall too (SM_G_TALL_RIGHT), no spills in either (168 / 160 VGPRs).  A dead end: off by default, kept
 // as an A/B switch (profiles/microbench/r04_guided_tall_ab.txt).
+// SM_G_TALL=2: 96-row tiles on one 12-wave workgroup per CU (3, 3, 3, 3 waves on the SIMDs, the
+// occupancy of three 4-wave workgroups): P halo 64 x 116 / (44 x 96) = 1.76, A halo 1.36, 133 KB of LDS.
 #ifndef SM_G_TALL
 #define SM_G_TALL 0
 #endif
 template <int R>
 constexpr bool kGuidedTall = SM_G_TALL != 0 && R >= 1 && R <= 5;
+constexpr int kTallKind = SM_G_TALL;
 
-template <int R, bool ROLES = kGuidedRoles, bool TALL = false>
+// TALL: 0 = 32-row tiles on 4 waves, 1 = 48 rows on 6 waves, 2 = 96 rows on 12 waves
+template <int R, bool ROLES = kGuidedRoles, int TALL = 0>
 struct GeoF {
-    static constexpr int NT = TALL ? 384 : kT;               // threads per workgroup
+    static constexpr int NT = TALL == 2 ? 768 : TALL ? 384 : kT;   // threads per workgroup
     static constexpr int NWV = NT / 64;                      // waves per workgroup
     static constexpr int TW = 64 - 4 * R;
-    static constexpr int TH = TALL ? 48 : 32;
+    static constexpr int TH = TALL == 2 ? 96 : TALL ? 48 : 32;
     static constexpr int AW = TW + 2 * R;
     static constexpr int AH = TH + 2 * R;
     static constexpr int PH = TH + 4 * R;
@@ -121,7 +125,8 @@ struct GeoF {
     static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
     static constexpr int AHP = SV * RPW;                     // cs rows incl. the last wave's pad rows
     static constexpr int PHP = SV * RPW + 2 * R;             // staged P rows incl. pad rows (>= PH)
-    static constexpr int NSEG1 = NT / AH;                    // S1H segments per A row
+    // S1H segments per A row (6 at 96 rows: an odd SW1 for the bank-spread CS stride)
+    static constexpr int NSEG1 = TALL == 2 ? 6 : NT / AH;
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
     static constexpr int CSS0 = (NSEG1 * SW1 + 2 * R) > 64 ? (NSEG1 * SW1 + 2 * R) : 64;
@@ -141,7 +146,8 @@ struct GeoF {
                AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
     }
     static constexpr int CSS =
-        (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : TALL ? 81920 : 53248)) ? CSS_B : CSS_OLD;
+        (SW1 % 2 == 1 && lds_for(CSS_B) <= (TALL == 2 ? 163840 : R >= 6 ? 81920 : TALL ? 81920 : 53248)) ? CSS_B
+                                                                                                       : CSS_OLD;
     // mm is two float planes (sum a, sum b), rows of MSA floats.  S2V stores them lane-consecutively
     // (ds_write_addtid_b32, 2 LDS cycles per 64 lanes against 6 for a float2 ds_write_b64); S2H reads
     // its segment as ds_read_b64 pairs.  MSA = 2 (mod 4): the b64 reads of 32 lanes (32 rows, one
@@ -302,15 +308,16 @@ constexpr bool kGuidedTallRight = SM_G_TALL_RIGHT != 0 && kGuidedTall<R> && kRol
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
-static_assert(GeoF<5, true, true>::LDS <= 81920, "tall r = 5 tile: two workgroups per CU");
+static_assert(GeoF<5, true, 1>::LDS <= 81920, "tall r = 5 tile: two workgroups per CU");
+static_assert(GeoF<5, true, 2>::LDS <= 163840 && GeoF<1, true, 2>::LDS <= 163840, "96-row tile: one workgroup per CU");
 
 // right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
 constexpr float kRightScale = 16384.0f;
 constexpr float kRightMax = 8388607.0f;    // 2^23 - 1
 constexpr float kRightMin = -8388608.0f;   // -2^23
 
-template <int R, bool RIGHT, bool TALL = false>
-__global__ __launch_bounds__((TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
+template <int R, bool RIGHT, int TALL = 0>
+__global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
@@ -793,11 +800,11 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && kRolesRight<R>>::LDS;
     if (!gpart) {
         if constexpr (kGuidedTall<R>) {
-            using GT = GeoF<R, kGuidedRoles, true>;
+            using GT = GeoF<R, kGuidedRoles, kTallKind>;
             const int tyt = (H + GT::TH - 1) / GT::TH;
             const int64_t bt = (int64_t)tiles_x * tyt * batch;
             if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((guided_fused_kernel<R, false, true>), dim3((unsigned)bt), dim3(GT::NT),
+            hipLaunchKernelGGL((guided_fused_kernel<R, false, kTallKind>), dim3((unsigned)bt), dim3(GT::NT),
                                (size_t)GT::LDS, s, L, Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp,
                                out_pitch, ostride, tiles_x, tiles_x * tyt, nullptr, 0, keys);
             return hipGetLastError();
@@ -810,11 +817,11 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
     if constexpr (kGuidedTallRight<R>) {
-        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, true>;
+        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, 1>;
         const int tyt = (H + GT::TH - 1) / GT::TH;
         const int64_t bt = (int64_t)tiles_x * tyt * batch;
         if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((guided_fused_kernel<R, true, true>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
+        hipLaunchKernelGGL((guided_fused_kernel<R, true, 1>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
                            L, Rimg, W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x,
                            tiles_x * tyt, gpart, K, nullptr);
         hipError_t e = hipGetLastError();
@@ -837,7 +844,7 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
 
 template <int R>
 size_t partial_bytes(int W, int H, int D, int batch) {
-    using G = GeoF<R, false, kGuidedTallRight<R>>;
+    using G = GeoF<R, false, kGuidedTallRight<R> ? 1 : 0>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }
