@@ -305,6 +305,8 @@ constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && 
 #endif
 template <int R>
 constexpr bool kGuidedTallRight = SM_G_TALL_RIGHT != 0 && kGuidedTall<R> && kRolesRight<R> && R != 3;
+// the right view's tile kind when tall: SM_G_TALL_RIGHT's value (1: 48 rows, 2: 96 rows)
+constexpr int kTallRightKind = SM_G_TALL_RIGHT;
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
@@ -817,11 +819,11 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
     if constexpr (kGuidedTallRight<R>) {
-        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, 1>;
+        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, kTallRightKind>;
         const int tyt = (H + GT::TH - 1) / GT::TH;
         const int64_t bt = (int64_t)tiles_x * tyt * batch;
         if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((guided_fused_kernel<R, true, 1>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
+        hipLaunchKernelGGL((guided_fused_kernel<R, true, kTallRightKind>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
                            L, Rimg, W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x,
                            tiles_x * tyt, gpart, K, nullptr);
         hipError_t e = hipGetLastError();
@@ -844,7 +846,7 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
 
 template <int R>
 size_t partial_bytes(int W, int H, int D, int batch) {
-    using G = GeoF<R, false, kGuidedTallRight<R> ? 1 : 0>;
+    using G = GeoF<R, false, kGuidedTallRight<R> ? kTallRightKind : 0>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }
