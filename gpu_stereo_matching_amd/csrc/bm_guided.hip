@@ -317,6 +317,17 @@ static_assert(GeoF<5, true, 2>::LDS <= 163840 && GeoF<1, true, 2>::LDS <= 163840
 constexpr float kRightScale = 16384.0f;
 constexpr float kRightMax = 8388607.0f;    // 2^23 - 1
 constexpr float kRightMin = -8388608.0f;   // -2^23
+// Fused right view's keys (round 4, SM_G_RKEY=1): v_cvt_i32_f32(q * 2^22) with its low 8 bits replaced by
+// the position, i.e. floor(q * 2^14) above the position field.  The conversion saturates at |q| >= 512,
+// which is the old clamp, so a key costs a multiply, one v_min_f32 (a NaN scale, outputs outside the
+// tile or the image, becomes 4e9 and so the largest key), the convert and one v_and_or_b32, instead of
+// v_min_f32 + v_max_f32 + multiply + convert + v_lshl_or_b32 (min / max issue at half rate).
+// SM_G_RKEY=0: the clamped round-3 keys, (int)(q * 2^14) << 8 | position.
+#ifndef SM_G_RKEY
+#define SM_G_RKEY 1
+#endif
+constexpr bool kRkeySat = SM_G_RKEY != 0;
+constexpr float kRightScaleSat = 4194304.0f;   // 2^22
 
 template <int R, bool RIGHT, int TALL = 0>
 __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
@@ -459,10 +470,12 @@ __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesP
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
         if constexpr (RIGHT) {
-            rinv[o] = ok ? kRightScale / (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_nanf("");
+            rinv[o] = ok ? (kRkeySat ? kRightScaleSat : kRightScale) / (float)(win_count(x, R, W) * win_count(oy, R, H))
+                         : __builtin_nanf("");
             rk[o] = INT_MAX;
         }
     }
+
     // right-key chain: first / last segment of the row, this row's partial-key column in gpart
     const bool seg_first = h2s == 0, seg_last = h2s == 7;
     int* gdst = RIGHT ? gpart + ((int64_t)frame * tiles + t) * K * G::TH + h2r : nullptr;
@@ -667,8 +680,17 @@ __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesP
             if constexpr (RIGHT) {
                 // candidate for right pixel u = x - d (slot o): q = (N q) / N, fixed point, position
                 // 7 SW2 + o (the output column relative to this segment, see the file header)
-                const float qs = __builtin_fmaxf(__builtin_fminf(q * rinv[o], kRightMax), kRightMin);
-                const int key = ((int)qs << 8) | (7 * G::SW2 + o);
+                int key;
+                if constexpr (kRkeySat) {
+                    // NaN (outputs outside) -> 4e9 -> INT_MAX; the conversion saturates both ways
+                    const float qs = __builtin_fminf(q * rinv[o], 4.0e9f);
+                    int k;
+                    asm("v_cvt_i32_f32 %0, %1" : "=v"(k) : "v"(qs));
+                    key = (k & ~0xFF) | (7 * G::SW2 + o);
+                } else {
+                    const float qs = __builtin_fmaxf(__builtin_fminf(q * rinv[o], kRightMax), kRightMin);
+                    key = ((int)qs << 8) | (7 * G::SW2 + o);
+                }
                 rk[o] = key < rk[o] ? key : rk[o];
             }
             sa -= va[o];
