@@ -273,8 +273,13 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
         for (int o = 0; o < G::NQ; ++o) best[h][o] = a.seed_key;
 
     const int xmax_tile = min(x0 + G::TW, W) - 1;
-    const bool d_edge = (a.valid_mode == 0 ? (xmax_tile + d_hi - 1 > W) : (d_hi - 1 > x0)) ||
-                        (RIGHT && x0 + G::TW > W);
+    // the masked phase H (the validity d <= W - x of Device.cu:44, or d <= x mirrored; a partial final
+    // pair; the right view's outputs past W) runs only for the pairs that need it.  d_free is the largest
+    // d valid for every output of the tile, so a pair (d, d + 1) masks nothing while d + 1 <= d_free
+    // (round 4: an edge tile's small-d pairs take the unmasked path; until then every pair of an edge tile
+    // was masked)
+    const int d_free = a.valid_mode == 0 ? W - xmax_tile : x0;
+    const bool r_out = RIGHT && x0 + G::TW > W;
     const bool col_in = (c >= 0) && (c < W);
     const int npairs = dspan >> 1;                 // multiple of 4
     const int p_lo = (wave * npairs) / NW;
@@ -299,7 +304,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
             sb[k] = m1 ? sel_b(k) : kSelW;
         }
         const uint32_t dsel = (uint32_t)(d & 0xFF) | ((uint32_t)((d + 1) & 0xFF) << 8);
-        const bool dm = d_edge || (d + 1 >= d_hi);
+        const bool dm = r_out || (d + 1 > d_free) || (d + 1 >= d_hi);
         uint32_t T = 0u, Tprev[2 * R + 1];
 #pragma unroll
         for (int h = 0; h < kNB; ++h) {
