@@ -1,6 +1,6 @@
 // bm_aux.hip — byte-streaming kernels around the matcher: key finalisation (multi-GPU
 // d-slice reduction), horizontal mirror (right view), left-right consistency check.
-// All are HBM-bound elementwise passes: 16 pixels per thread, 16-B loads where aligned.
+// All are HBM-bound elementwise passes (the LR check: one row per block, 4 pixels per thread).
 #include "bm_common.h"
 
 namespace sm {
@@ -55,6 +55,62 @@ __global__ __launch_bounds__(256) void lr_check_kernel(const uint8_t* ld, int lp
     if (right_out) right_out[(int64_t)f * astride + (int64_t)y * apitch + x] = rrow[mirrored ? W - 1 - x : x];
 }
 
+// The same check with one block per (row, frame) (round 4): the right row is staged in LDS, so its
+// gathers dR(x - d) stay on chip, and each thread takes 4 pixels with dword loads and stores when the
+// rows are 4-byte aligned (bytes otherwise, and for a row's last W mod 4 pixels).  The byte-per-thread
+// kernel above took 6.2 us per 1080p frame for ~8 MB of traffic (guided + LR, 32-frame launches).
+__global__ __launch_bounds__(256) void lr_check_row_kernel(const uint8_t* ld, int lpitch, int64_t lstride,
+                                                           const uint8_t* __restrict__ rd, int rpitch, int64_t rstride,
+                                                           int mirrored, int W, uint8_t* out, int opitch,
+                                                           int64_t ostride, uint8_t* __restrict__ right_out,
+                                                           uint8_t* __restrict__ mask_out, int apitch,
+                                                           int64_t astride) {
+    extern __shared__ uint8_t rs[];   // the right row, W bytes (+3 pad)
+    const int y = blockIdx.x, f = blockIdx.y;
+    const uint8_t* lrow = ld + (int64_t)f * lstride + (int64_t)y * lpitch;
+    const uint8_t* rrow = rd + (int64_t)f * rstride + (int64_t)y * rpitch;
+    uint8_t* orow = out + (int64_t)f * ostride + (int64_t)y * opitch;
+    uint8_t* mrow = mask_out ? mask_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    uint8_t* rorow = right_out ? right_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
+    const bool vec = ((reinterpret_cast<uintptr_t>(lrow) | reinterpret_cast<uintptr_t>(rrow) |
+                       reinterpret_cast<uintptr_t>(orow) | reinterpret_cast<uintptr_t>(mrow) |
+                       reinterpret_cast<uintptr_t>(rorow)) & 3) == 0;
+    const int W4 = vec ? (W & ~3) : 0;   // pixels taken 4 at a time
+    for (int i = threadIdx.x * 4; i < W4; i += blockDim.x * 4)
+        *reinterpret_cast<uint32_t*>(rs + i) = *reinterpret_cast<const uint32_t*>(rrow + i);
+    for (int i = W4 + threadIdx.x; i < W; i += blockDim.x) rs[i] = rrow[i];
+    __syncthreads();
+    auto one = [&](int x, int d) -> uint32_t {   // checked d (low byte) | mask << 8 | dR(x) << 16
+        int occ = 1;
+        if (x - d >= 0) {
+            const int u = x - d;
+            const int diff = d - (int)rs[mirrored ? W - 1 - u : u];
+            occ = (d == 0) || diff > 1 || diff < -1;
+        }
+        return (occ ? 0u : (uint32_t)d) | ((uint32_t)!occ << 8) | ((uint32_t)rs[mirrored ? W - 1 - x : x] << 16);
+    };
+    for (int x = threadIdx.x * 4; x < W4; x += blockDim.x * 4) {
+        const uint32_t dl = *reinterpret_cast<const uint32_t*>(lrow + x);
+        uint32_t o = 0, m = 0, r = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t v = one(x + b, (int)((dl >> (8 * b)) & 0xFFu));
+            o |= (v & 0xFFu) << (8 * b);
+            m |= ((v >> 8) & 0xFFu) << (8 * b);
+            r |= (v >> 16) << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(orow + x) = o;
+        if (mrow) *reinterpret_cast<uint32_t*>(mrow + x) = m;
+        if (rorow) *reinterpret_cast<uint32_t*>(rorow + x) = r;
+    }
+    for (int x = W4 + threadIdx.x; x < W; x += blockDim.x) {
+        const uint32_t v = one(x, lrow[x]);
+        orow[x] = (uint8_t)(v & 0xFFu);
+        if (mrow) mrow[x] = (uint8_t)(v >> 8);
+        if (rorow) rorow[x] = (uint8_t)(v >> 16);
+    }
+}
+
 // acc[i] = min(acc[i], src[i]), signed (box keys are < 2^31, guided keys carry a signed cost): the
 // MIN of an RCCL reduce-scatter, for the d-slice split rehearsed on one device (sm_dslice_rehearse_u8)
 __global__ __launch_bounds__(256) void min_keys_kernel(int* __restrict__ acc, const int* __restrict__ src, int64_t n) {
@@ -88,6 +144,13 @@ hipError_t launch_lr_check(const uint8_t* left_disp, int lpitch, int64_t lstride
                            int rpitch, int64_t rstride, int right_mirrored, int W, int H, int batch, uint8_t* out,
                            int opitch, int64_t ostride, uint8_t* right_out, uint8_t* mask_out, int aux_pitch,
                            int64_t aux_stride, hipStream_t s) {
+    if (W <= 0 || H <= 0 || batch <= 0) return hipSuccess;
+    if (W <= 16384) {   // the right row in LDS
+        hipLaunchKernelGGL(lr_check_row_kernel, dim3((unsigned)H, (unsigned)batch), dim3(256), (size_t)((W + 3) & ~3), s,
+                           left_disp, lpitch, lstride, right_disp, rpitch, rstride, right_mirrored, W, out, opitch,
+                           ostride, right_out, mask_out, aux_pitch, aux_stride);
+        return hipGetLastError();
+    }
     dim3 grid((W + 255) / 256, H, batch);
     hipLaunchKernelGGL(lr_check_kernel, grid, dim3(256), 0, s, left_disp, lpitch, lstride, right_disp, rpitch, rstride,
                        right_mirrored, W, out, opitch, ostride, right_out, mask_out, aux_pitch, aux_stride);
