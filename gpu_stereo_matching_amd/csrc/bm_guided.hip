@@ -771,7 +771,10 @@ __global__ __launch_bounds__(256) void guided_keys_to_disp_kernel(const int* __r
 // Right view of the fused pass: for each right pixel u of a tile row band, the minimum key over the
 // tiles whose chain emitted u (k = x0 + SPAN - 1 - u in [0, K)), decoded to d = x0 + position - u.
 // Block = 64 columns x the 32 rows of one tile band; reads are 128-B rows of gpart ([k][row]).
-template <int TH>
+// MAXT >= the most tiles covering one u, (K + TW - 1) / TW + 1: a fixed trip count, so every key load of
+// an entry issues before the first compare (round 4; the loop over the covering tiles had each load wait
+// for the compare before it)
+template <int TH, int MAXT>
 __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __restrict__ gpart, int tiles_x, int tiles,
                                                                   int TW, int SPAN, int K, int W, int H,
                                                                   uint8_t* __restrict__ right, int rpitch,
@@ -787,18 +790,23 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
             const int n = u - SPAN + 1;
             const int tlo = n <= 0 ? 0 : (n + TW - 1) / TW;
             const int thi = min(tiles_x - 1, (u - SPAN + K) / TW);
+            int key[MAXT];
+#pragma unroll
+            for (int m = 0; m < MAXT; ++m) {
+                const int tx = tlo + m;
+                key[m] = tx <= thi ? base[((int64_t)tx * K + (tx * TW + SPAN - 1 - u)) * TH + j] : INT_MAX;
+            }
             // keys order (cost, column) within a tile only: across tiles compare the cost field,
             // strict <, in ascending tile order, so equal costs keep the smaller column = smaller d
-            int best = base[((int64_t)tlo * K + (tlo * TW + SPAN - 1 - u)) * TH + j], bx = tlo * TW;
-            for (int tx = tlo + 1; tx <= thi; ++tx) {
-                const int k = tx * TW + SPAN - 1 - u;
-                const int key = base[((int64_t)tx * K + k) * TH + j];
-                if ((key >> 8) < (best >> 8)) {
-                    best = key;
-                    bx = tx * TW;
+            int best = key[0], bm = 0;
+#pragma unroll
+            for (int m = 1; m < MAXT; ++m) {
+                if ((key[m] >> 8) < (best >> 8)) {
+                    best = key[m];
+                    bm = m;
                 }
             }
-            dr = bx + (best & 0xFF) - u;
+            dr = (tlo + bm) * TW + (best & 0xFF) - u;
         }
         band[j][ul] = (uint8_t)dr;
     }
@@ -809,6 +817,25 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
         const int y = ty * TH + j, u = u0 + ul;
         if (y < H && u < W) Rf[(int64_t)y * rpitch + u] = band[j][ul];
     }
+}
+
+// the reduce with the smallest instantiated MAXT >= (K + TW - 1) / TW + 1 (D <= 256, TW >= 36: <= 10)
+template <int TH>
+hipError_t launch_right_reduce(const int* gpart, int tiles_x, int tiles_y, int batch, int TW, int span, int K, int W,
+                               int H, uint8_t* right, int rpitch, int64_t rstride, hipStream_t s) {
+    const int need = (K + TW - 1) / TW + 1;
+    const dim3 grid((unsigned)((W + 63) / 64), (unsigned)tiles_y, (unsigned)batch);
+    const int tiles = tiles_x * tiles_y;
+#define SM_RIGHT_REDUCE(M)                                                                                      \
+    hipLaunchKernelGGL((guided_right_reduce_kernel<TH, M>), grid, dim3(256), 0, s, gpart, tiles_x, tiles, TW, span, K, \
+                       W, H, right, rpitch, rstride)
+    if (need <= 4) SM_RIGHT_REDUCE(4);
+    else if (need <= 6) SM_RIGHT_REDUCE(6);
+    else if (need <= 8) SM_RIGHT_REDUCE(8);
+    else if (need <= 10) SM_RIGHT_REDUCE(10);
+    else return hipErrorInvalidValue;
+#undef SM_RIGHT_REDUCE
+    return hipGetLastError();
 }
 
 template <int R>
@@ -850,20 +877,14 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
                            tiles_x * tyt, gpart, K, nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(guided_right_reduce_kernel<GT::TH>, dim3((unsigned)((W + 63) / 64), (unsigned)tyt,
-                           (unsigned)batch), dim3(256), 0, s, gpart, tiles_x, tiles_x * tyt, G::TW, span, K, W, H,
-                           right, rpitch, rstride);
-        return hipGetLastError();
+        return launch_right_reduce<GT::TH>(gpart, tiles_x, tyt, batch, G::TW, span, K, W, H, right, rpitch, rstride, s);
     }
     hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), lds_right, s, L, Rimg,
                        W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
                        K, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(guided_right_reduce_kernel<G::TH>, dim3((unsigned)((W + 63) / 64), (unsigned)tiles_y,
-                       (unsigned)batch), dim3(256), 0, s, gpart, tiles_x, tiles_x * tiles_y, G::TW, span, K, W, H,
-                       right, rpitch, rstride);
-    return hipGetLastError();
+    return launch_right_reduce<G::TH>(gpart, tiles_x, tiles_y, batch, G::TW, span, K, W, H, right, rpitch, rstride, s);
 }
 
 template <int R>
