@@ -204,7 +204,8 @@ class BlockMatcher:
               d < max_level -> tree aggregation on the left view's colour tree -> WTA -> 7x7 median -> x scale;
           1 = ST-2 (stereo_disparity_iteration, :91-160): first-pass left / right maps on colour trees of
               each view, the left-right check, then a colour + depth tree on the left view.
-        Cost, filter, WTA, median and LR check on the GPU, the trees on the host (as the reference)."""
+        Cost, filter, WTA, median, LR check and the trees' BFS on the GPU; segment_graph's passes on the
+        host (sequential, as the reference's)."""
         Lb = np.ascontiguousarray(left_bgr, dtype=np.uint8)
         Rb = np.ascontiguousarray(right_bgr, dtype=np.uint8)
         if Lb.ndim != 3 or Lb.shape[2] != 3 or Lb.shape != Rb.shape:
@@ -219,10 +220,23 @@ class BlockMatcher:
         return out
 
     def segment_tree_stats(self) -> Tuple[float, float, int]:
-        """(host tree-build ms, whole-call ms, BFS levels of the last tree) of the last segment_tree call."""
+        """(tree-build ms, whole-call ms, BFS levels of the last tree) of the last segment_tree call."""
         t, a, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
         _capi.check(self._lib.sm_last_segment_tree_stats(self._h, ctypes.byref(t), ctypes.byref(a), ctypes.byref(n)))
         return t.value, a.value, n.value
+
+    def segment_tree_arrays(self, width: int, height: int) -> dict:
+        """The last segment_tree call's last tree in BFS order (sm_last_segment_tree_arrays): rank, parent,
+        first, child, lev (levels + 1 offsets) and pdist, for a width x height frame."""
+        P = int(width) * int(height)
+        ints = np.empty(5 * P + 2, np.int32)
+        pdist = np.empty(P, np.uint8)
+        n = ctypes.c_int()
+        _capi.check(self._lib.sm_last_segment_tree_arrays(self._h, ints.ctypes.data, ints.size, pdist.ctypes.data,
+                                                          pdist.size, ctypes.byref(n)))
+        return {"rank": ints[:P].copy(), "parent": ints[P:2 * P].copy(), "first": ints[2 * P:3 * P].copy(),
+                "child": ints[3 * P:4 * P].view(np.uint32).copy(), "lev": ints[4 * P:4 * P + n.value + 1].copy(),
+                "pdist": pdist}
 
     def cvt_color(self, bgr) -> np.ndarray:
         """cvtColor_gpu (Device.cuh:52) on host memory: HxWx3|4 uint8 BGR(A) -> gray, OpenCV 2.4 weights."""

@@ -41,7 +41,8 @@ EXPORTED = (
     "sm_create_group", "sm_destroy_group", "sm_group_size", "sm_group_set_param_f", "sm_group_block_match_u8",
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
     "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_segment_tree_refined_bgr_u8",
-    "sm_last_segment_tree_stats", "sm_host_alloc", "sm_host_free", "sm_dslice_plan", "sm_dslice_rehearse_u8",
+    "sm_last_segment_tree_stats", "sm_last_segment_tree_arrays", "sm_host_alloc", "sm_host_free",
+    "sm_dslice_plan", "sm_dslice_rehearse_u8",
 )
 
 
@@ -107,6 +108,7 @@ def load(path: str = LIB_PATH):
     L.sm_segment_tree_refined_bgr_u8.argtypes = [vp, vp, vp, i, i, i, i, i, ctypes.c_float, vp, i]
     L.sm_last_segment_tree_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                              ctypes.POINTER(ctypes.c_int)]
+    L.sm_last_segment_tree_arrays.argtypes = [vp, vp, i64, vp, i64, ctypes.POINTER(ctypes.c_int)]
     L.sm_stereo_rectify.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp]
     L.sm_init_rectify_map_device.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i, vp]
     L.sm_init_rectify_map.argtypes = [vp, vp, vp, i, vp, vp, i, i, vp, vp, i]

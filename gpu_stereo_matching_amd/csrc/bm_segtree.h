@@ -16,6 +16,14 @@ struct StWorkspace {
     uint8_t* tree_b = nullptr; // P per tree: distance to the parent
     float* table = nullptr;    // 256 per tree: exp(-i / (255 sigma))
     int* task = nullptr;       // per tree: the wave filter's level tasks (int4 each), up to 2 * (P + levels)
+    int* bfs[2] = {nullptr, nullptr};   // the device BFS's scratch per tree slot (round 4, bm_segtree.hip: bfs_scratch)
+    hipStream_t side = nullptr;         // ST-2: the right view's BFS runs on it beside the left's
+    hipEvent_t side_ev = nullptr;       // recorded on `side` after that BFS
+    int* node = nullptr;       // P per tree: BFS index -> pixel (the WTA's output order)
+    size_t node_n = 0;
+    int* h_hdr = nullptr;      // page-locked: per tree slot {levels, widest level, up tasks, down tasks}
+    hipEvent_t bfs_ev = nullptr;   // recorded after the device BFS's header copies
+    int last_P = 0, last_nlev = 0; // tree slot 0 of the last call (sm_last_segment_tree_arrays)
     uint32_t* sortbuf = nullptr;   // edge sort: keys and values (2 x 2 nE), digit counts, sorted edges (3 nE)
     void* h_edges[2] = {nullptr, nullptr};   // page-locked host copies of sorted edges (12 B each), 2 trees
     // page-locked host trees (round 4), one per tree slot: ints in the device slot's layout (rank, parent,
@@ -27,7 +35,8 @@ struct StWorkspace {
     static constexpr int kEdgeChunks = 4;
     hipEvent_t edge_ev[2][kEdgeChunks] = {};
     int edge_chunk[2] = {0, 0};   // edges per chunk of each slot's last download
-    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0, sortbuf_n = 0;
+    size_t w8_n = 0, grad_n = 0, vol_n = 0, tree_i_n = 0, tree_b_n = 0, table_n = 0, task_n = 0, sortbuf_n = 0,
+           bfs_n[2] = {0, 0};
     size_t h_edges_n[2] = {0, 0}, h_tree_n[2] = {0, 0};
     ~StWorkspace();
     void release();
@@ -35,7 +44,7 @@ struct StWorkspace {
 
 struct StStats {
     int levels = 0;        // BFS levels of the (last) tree
-    float tree_ms = 0.f;   // host time of the tree builds
+    float tree_ms = 0.f;   // time of the tree builds (host lists + the BFS, until its level count is back)
 };
 
 // stereo_disparity_normal (StereoDisparity.cpp:57-89) on device BGR frames (3 bytes per pixel, row

@@ -399,12 +399,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
          });
 }
 
-// GetDisparity_WTA (StereoHelper.cpp:131-154): strict < from d = 0; times scale, saturated
-__global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F, const int* __restrict__ rank, int P,
-                                                     int D, int scale, uint8_t* __restrict__ out) {
+// node[i] = the pixel at BFS index i (the inverse of rank)
+__global__ __launch_bounds__(kST) void st_node_kernel(const int* __restrict__ rank, int P, int* __restrict__ node) {
     const int p = blockIdx.x * kST + threadIdx.x;
     if (p >= P) return;
     const int i = rank[p];
+    if ((unsigned)i < (unsigned)P) node[i] = p;
+}
+
+// GetDisparity_WTA (StereoHelper.cpp:131-154): strict < from d = 0; times scale, saturated.  One thread
+// per BFS index, so the D cost reads of a wave are coalesced (round 4: per pixel, they were gathers
+// through rank, 62 -> 9 us for Art at D = 60); the result goes to its pixel.
+__global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F, const int* __restrict__ node, int P,
+                                                     int D, int scale, uint8_t* __restrict__ out) {
+    const int i = blockIdx.x * kST + threadIdx.x;
+    if (i >= P) return;
     float v = F[i];
     int m = 0;
     for (int d = 1; d < D; ++d) {
@@ -414,7 +423,8 @@ __global__ __launch_bounds__(kST) void st_wta_kernel(const float* __restrict__ F
             m = d;
         }
     }
-    out[p] = (uint8_t)min(m * scale, 255);
+    const int p = node[i];
+    if ((unsigned)p < (unsigned)P) out[p] = (uint8_t)min(m * scale, 255);
 }
 
 // ---- the edge order on the GPU: SegmentTree.cpp:44-69's edges sorted by edge::operator< (weight, then
@@ -468,18 +478,29 @@ __global__ __launch_bounds__(kST) void st_edge_keys_kernel(const uint8_t* __rest
     }
 }
 
-// one radix pass: single-wave blocks of kRxIPB consecutive items, 64 per round
+// one radix pass: single-wave blocks of R * 64 consecutive items, 64 per round (the edge sort: kRxRounds;
+// the device BFS's scans and depth sort: kScRounds, 4x the waves for its P-item passes)
 constexpr int kRxRounds = 32;
 constexpr int kRxIPB = 64 * kRxRounds;
+constexpr int kScRounds = 8;
+constexpr int kScIPB = 64 * kScRounds;
 
+// gate (the device BFS's sort of depths, bm_segtree.hip st_radix_passes_run): a pass with shift > 0 whose
+// digit is 0 for every key (gate[4] = the largest key) does nothing; null for the edge sort
+__device__ __forceinline__ bool st_rx_skip(const int* gate, int shift) {
+    return gate && shift > 0 && (gate[4] >> shift) == 0;
+}
+
+template <int R>
 __global__ __launch_bounds__(64) void st_rx_hist_kernel(const uint32_t* __restrict__ keys, int n, int shift,
-                                                        uint32_t* __restrict__ hist, int nb) {
+                                                        uint32_t* __restrict__ hist, int nb, const int* gate) {
+    if (st_rx_skip(gate, shift)) return;
     __shared__ uint32_t h[256];
     const int lane = threadIdx.x, blk = blockIdx.x;
     for (int k = lane; k < 256; k += 64) h[k] = 0;
     __syncthreads();
-    for (int r = 0; r < kRxRounds; ++r) {
-        const int i = blk * kRxIPB + r * 64 + lane;
+    for (int r = 0; r < R; ++r) {
+        const int i = blk * R * 64 + r * 64 + lane;
         if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFFu], 1u);
     }
     __syncthreads();
@@ -498,7 +519,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 __global__ __launch_bounds__(64) void st_rx_scan_rows_kernel(uint32_t* __restrict__ hist, int nb,
-                                                             uint32_t* __restrict__ total) {
+                                                             uint32_t* __restrict__ total, const int* gate, int shift) {
+    if (st_rx_skip(gate, shift)) return;
     const int lane = threadIdx.x, dg = blockIdx.x;
     uint32_t* row = hist + (size_t)dg * nb;
     uint32_t run = 0;
@@ -511,7 +533,8 @@ __global__ __launch_bounds__(64) void st_rx_scan_rows_kernel(uint32_t* __restric
     }
     if (lane == 0) total[dg] = run;
 }
-__global__ __launch_bounds__(64) void st_rx_scan_bases_kernel(uint32_t* __restrict__ total) {
+__global__ __launch_bounds__(64) void st_rx_scan_bases_kernel(uint32_t* __restrict__ total, const int* gate, int shift) {
+    if (st_rx_skip(gate, shift)) return;
     const int lane = threadIdx.x;
     uint32_t run = 0;
     for (int d0 = 0; d0 < 256; d0 += 64) {
@@ -526,19 +549,20 @@ __global__ __launch_bounds__(64) void st_rx_scan_bases_kernel(uint32_t* __restri
 // same digit before it in the block (earlier rounds: the running counts cnt; this round: the lanes below
 // it whose 8 digit bits all agree, from 8 ballots).  FINAL: write the edge records {a, b, w} instead of
 // keys and values.
-template <bool FINAL, bool DEPTH>
+template <bool FINAL, bool DEPTH, int R = kRxRounds>
 __global__ __launch_bounds__(64) void st_rx_scatter_kernel(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                            int n, int shift, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ bases, int nb,
                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                           st_host::Edge* __restrict__ eout, int W) {
+                                                           st_host::Edge* __restrict__ eout, int W, const int* gate) {
+    if (st_rx_skip(gate, shift)) return;
     __shared__ uint32_t cnt[256];
     const int lane = threadIdx.x, blk = blockIdx.x;
     for (int k = lane; k < 256; k += 64) cnt[k] = bases[k] + hist[(size_t)k * nb + blk];
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (int r = 0; r < kRxRounds; ++r) {
-        const int i = blk * kRxIPB + r * 64 + lane;
+    for (int r = 0; r < R; ++r) {
+        const int i = blk * R * 64 + r * 64 + lane;
         const bool valid = i < n;
         const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
         const uint32_t dg = (k >> shift) & 0xFFu;
@@ -566,6 +590,362 @@ __global__ __launch_bounds__(64) void st_rx_scatter_kernel(const uint32_t* __res
             }
         }
     }
+}
+
+// ---- the BFS order on the GPU (round 4) ----
+// The host keeps segment_graph's two passes (sequential: every join's threshold depends on the joins
+// before it) and hands over the neighbour lists (st_host::AdjRec, 8 B per pixel: four distance bytes,
+// four 2-bit directions, the count).  The BFS of SegmentTree.cpp:97-130 (FIFO from pixel 0, a node's
+// children in list order) follows from them without walking the levels one by one:
+//  1. an Euler tour of the tree (arc p -> q continues from q to the neighbour after p in q's list,
+//     cyclically), ranked by pointer jumping (Wyllie), roots the tree: u is v's parent iff arc u -> v
+//     comes before v -> u, and v's subtree has (dist(u -> v) - dist(v -> u) + 1) / 2 nodes, dist being
+//     the number of arcs after an arc;
+//  2. a node's children in list order (the parent skipped) get the preorder offsets 1 + the sizes of
+//     their earlier siblings.  A prefix sum along the tour of {+1, +offset(v)} on each arc into v and
+//     {-1, -offset(v)} on each arc out of v's subtree leaves, at the arc into v, exactly the terms of v's
+//     ancestors and v (a finished subtree cancels, whatever the tour's order): v's depth and preorder
+//     number;
+//  3. in a FIFO BFS the nodes of one level come in preorder (by induction over the levels: nodes with
+//     different parents follow their parents' order, whose subtrees are disjoint preorder intervals in
+//     that order; siblings follow the list order), so the BFS order is the preorder stably sorted by
+//     depth (the edge sort's radix passes, those above the deepest level's top bit skipped);
+//  4. rank, child words and level offsets from that order; first = 1 + the exclusive scan of the child
+//     counts (the BFS appends a node's children at the running end), and each node writes its children's
+//     parent index and distance byte there; the wave filter's tasks (wave_tasks' layout) from a scan of
+//     the per-level task counts.
+// The same arrays as st_host::bfs_tree, bit for bit (tests/test_gpu_segtree.py compares both).
+static_assert(sizeof(st_host::AdjRec) == 8, "AdjRec is read as a uint2 {d, dir | n << 16}");
+
+__device__ __forceinline__ int st_nb(int p, uint32_t dir, int k, int W) {
+    const uint32_t c = (dir >> (2 * k)) & 3u;
+    return c == 0 ? p - 1 : c == 1 ? p + 1 : c == 2 ? p - W : p + W;
+}
+
+// arcs: slot k of pixel p is arc 4 p + k {next arc of the tour, 1}; the arc into arc 0 (pixel 0 to its
+// first neighbour, where the tour starts) ends it {-1, 0}, and so do the unused slots; rev = the reverse
+// arc (an unused slot: itself)
+__global__ __launch_bounds__(kST) void st_arc_kernel(const uint2* __restrict__ adj, int P, int W,
+                                                     int2* __restrict__ arc, int* __restrict__ rev) {
+    const int p = blockIdx.x * kST + threadIdx.x;
+    if (p >= P) return;
+    const uint2 a = adj[p];
+    const int n = (int)(a.y >> 16);
+    const uint32_t dir = a.y & 0xFFFFu;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int2 r = make_int2(-1, 0);
+        int rv = 4 * p + k;
+        if (k < n) {
+            const int q = st_nb(p, dir, k, W);
+            const uint2 b = adj[q];
+            const int nq = (int)(b.y >> 16);
+            const uint32_t back = ((dir >> (2 * k)) & 3u) ^ 1u, dq = b.y & 0xFFFFu;
+            int j = -1;
+#pragma unroll
+            for (int z = 0; z < 4; ++z)
+                if (z < nq && ((dq >> (2 * z)) & 3u) == back) j = z;
+            if (j >= 0) {
+                rv = 4 * q + j;
+                const int nx = 4 * q + (j + 1 == nq ? 0 : j + 1);
+                if (nx != 0) r = make_int2(nx, 1);
+            }
+        }
+        arc[4 * p + k] = r;
+        rev[4 * p + k] = rv;
+    }
+}
+
+// one pointer-jumping step: {next, count} -> {next of next, count + its count}
+__global__ __launch_bounds__(kST) void st_list_rank_kernel(const int2* __restrict__ in, int2* __restrict__ out, int n) {
+    const int a = blockIdx.x * kST + threadIdx.x;
+    if (a >= n) return;
+    int2 v = in[a];
+    if (v.x >= 0) {
+        const int2 w = in[v.x];
+        v = make_int2(w.x, v.y + w.y);
+    }
+    out[a] = v;
+}
+
+// parent slot (4: the root) and subtree size of every pixel from the ranked tour
+__global__ __launch_bounds__(kST) void st_root_kernel(const uint2* __restrict__ adj, const int2* __restrict__ rk,
+                                                      const int* __restrict__ rev, int P, int* __restrict__ psl,
+                                                      int* __restrict__ size) {
+    const int p = blockIdx.x * kST + threadIdx.x;
+    if (p >= P) return;
+    int slot = 4, sz = P;
+    if (p != 0) {
+        const int n = (int)(adj[p].y >> 16);
+        for (int k = 0; k < n; ++k) {
+            const int da = rk[4 * p + k].y, db = rk[rev[4 * p + k]].y;
+            if (db > da) {   // the arc into p comes first: its other end is the parent
+                slot = k;
+                sz = (db - da + 1) >> 1;
+            }
+        }
+    }
+    psl[p] = slot;
+    size[p] = sz;
+}
+
+// every node writes its children's preorder offsets and its child word (count | distance bytes in list
+// order, as bfs_tree's)
+__global__ __launch_bounds__(kST) void st_child_kernel(const uint2* __restrict__ adj, const int* __restrict__ psl,
+                                                       const int* __restrict__ size, int P, int W,
+                                                       int* __restrict__ offs, uint32_t* __restrict__ chw) {
+    const int p = blockIdx.x * kST + threadIdx.x;
+    if (p >= P) return;
+    const uint2 a = adj[p];
+    const int n = (int)(a.y >> 16), ps = psl[p];
+    int run = 1;
+    uint32_t ch = 0, m = 0;
+    for (int k = 0; k < n; ++k) {
+        if (k == ps) continue;
+        const int c = st_nb(p, a.y & 0xFFFFu, k, W);
+        const uint32_t dis = (a.x >> (8 * k)) & 0xFFu;
+        offs[c] = run;
+        run += size[c];
+        ch |= dis << (8 * (m + 1));
+        ++m;
+    }
+    chw[p] = ch | m;
+    if (p == 0) offs[0] = 0;
+}
+
+// {depth, preorder} weights of the arcs in tour order (position = L - 1 - dist, L = 2 (P - 1) arcs):
+// into a child {+1, +offset}, to the parent {-1, -offset}; tv = the child an arc enters, else -1
+struct U2 {
+    uint32_t a, b;
+};
+__device__ __forceinline__ U2 operator+(U2 x, U2 y) { return U2{x.a + y.a, x.b + y.b}; }
+__device__ __forceinline__ U2 operator-(U2 x, U2 y) { return U2{x.a - y.a, x.b - y.b}; }
+__global__ __launch_bounds__(kST) void st_tour_kernel(const uint2* __restrict__ adj, const int2* __restrict__ rk,
+                                                      const int* __restrict__ psl, const int* __restrict__ offs, int P,
+                                                      int W, U2* __restrict__ tw, int* __restrict__ tv) {
+    const int p = blockIdx.x * kST + threadIdx.x;
+    if (p >= P) return;
+    const uint2 a = adj[p];
+    const int n = (int)(a.y >> 16), ps = psl[p], L = 2 * (P - 1);
+    for (int k = 0; k < n; ++k) {
+        const int pos = L - 1 - rk[4 * p + k].y;
+        if ((unsigned)pos >= (unsigned)L) continue;
+        if (k == ps) {
+            tw[pos] = U2{~0u, (uint32_t)(-offs[p])};
+            tv[pos] = -1;
+        } else {
+            const int q = st_nb(p, a.y & 0xFFFFu, k, W);
+            tw[pos] = U2{1u, (uint32_t)offs[q]};
+            tv[pos] = q;
+        }
+    }
+}
+
+// wave-wide inclusive scans of uint32_t / U2 (the U2 halves wrap independently: partial sums of the
+// tour's weights go negative)
+__device__ __forceinline__ uint32_t shfl_up_v(uint32_t v, int off) { return __shfl_up(v, off, 64); }
+__device__ __forceinline__ U2 shfl_up_v(U2 v, int off) { return U2{__shfl_up(v.a, off, 64), __shfl_up(v.b, off, 64)}; }
+__device__ __forceinline__ uint32_t shfl_v(uint32_t v, int l) { return __shfl(v, l, 64); }
+__device__ __forceinline__ U2 shfl_v(U2 v, int l) { return U2{__shfl(v.a, l, 64), __shfl(v.b, l, 64)}; }
+template <class V>
+__device__ __forceinline__ V wave_scan_v(V v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const V u = shfl_up_v(v, off);
+        if (lane >= off) v = v + u;
+    }
+    return v;
+}
+
+// exclusive scan in blocks of kScIPB items, one wave each: the blocks' totals (st_scan_sums_kernel), one
+// wave over the totals (st_scan_rows_kernel, also writing the grand total), then the items with their
+// block's base (st_scan_apply_kernel: dst(i, exclusive prefix, item))
+template <class V, class Src>
+__global__ __launch_bounds__(64) void st_scan_sums_kernel(Src src, int n, V* __restrict__ sums) {
+    const int lane = threadIdx.x, blk = blockIdx.x;
+    V t{};
+    for (int r = 0; r < kScRounds; ++r) {
+        const int i = blk * kScIPB + r * 64 + lane;
+        if (i < n) t = t + src(i);
+    }
+    t = wave_scan_v(t, lane);
+    if (lane == 63) sums[blk] = t;
+}
+template <class V>
+__global__ __launch_bounds__(64) void st_scan_rows_kernel(V* __restrict__ sums, int nb, V* __restrict__ total) {
+    const int lane = threadIdx.x;
+    V run{};
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        const V c = b < nb ? sums[b] : V{};
+        const V inc = wave_scan_v(c, lane);
+        if (b < nb) sums[b] = run + inc - c;
+        run = run + shfl_v(inc, 63);
+    }
+    if (lane == 0 && total) *total = run;
+}
+template <class V, class Src, class Dst>
+__global__ __launch_bounds__(64) void st_scan_apply_kernel(Src src, int n, const V* __restrict__ sums, Dst dst) {
+    const int lane = threadIdx.x, blk = blockIdx.x;
+    V run = sums[blk];
+    for (int r = 0; r < kScRounds; ++r) {
+        const int i = blk * kScIPB + r * 64 + lane;
+        const V c = i < n ? src(i) : V{};
+        const V inc = wave_scan_v(c, lane);
+        if (i < n) dst(i, run + inc - c, c);
+        run = run + shfl_v(inc, 63);
+    }
+}
+
+// the tour's prefix sums -> the nodes in preorder (key = depth, value = pixel); hdr[4] = the largest depth
+struct StTourW {
+    const U2* tw;
+    __device__ U2 operator()(int i) const { return tw[i]; }
+};
+__global__ __launch_bounds__(64) void st_tour_apply_kernel(const U2* __restrict__ tw, const int* __restrict__ tv, int L,
+                                                           const U2* __restrict__ sums, uint32_t* __restrict__ keys,
+                                                           uint32_t* __restrict__ vals, int P, int* __restrict__ hdr) {
+    const int lane = threadIdx.x, blk = blockIdx.x;
+    U2 run = sums[blk];
+    uint32_t dmax = 0;
+    for (int r = 0; r < kScRounds; ++r) {
+        const int i = blk * kScIPB + r * 64 + lane;
+        const U2 c = i < L ? tw[i] : U2{0u, 0u};
+        const U2 inc = wave_scan_v(c, lane);
+        if (i < L) {
+            const int v = tv[i];
+            const U2 at = run + inc;   // inclusive: the arc into v counts v itself
+            if (v >= 0 && at.b < (uint32_t)P) {
+                keys[at.b] = at.a;
+                vals[at.b] = (uint32_t)v;
+                dmax = max(dmax, at.a);
+            }
+        }
+        run = run + shfl_v(inc, 63);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off, 64));
+    if (lane == 0) {
+        atomicMax(&hdr[4], (int)dmax);
+        if (blk == 0) {   // the root: depth 0, preorder 0
+            keys[0] = 0;
+            vals[0] = 0;
+        }
+    }
+}
+
+// radix passes above the deepest level's top bit are skipped (gate = hdr, gate[4] the largest depth):
+// the pass results alternate A -> B -> A.., so the sorted order is in B after an odd number of passes
+__device__ __forceinline__ int st_radix_passes_run(const int* hdr, int launched) {
+    int e = 0;
+    for (int k = 0; k < launched; ++k)
+        if (k == 0 || (hdr[4] >> (8 * k)) != 0) ++e;
+    return e;
+}
+
+// BFS-order arrays from the sorted nodes: rank, child words; lev[d] = the first node of depth d,
+// lev[levels] = P; hdr {levels, widest level = 1 (st_level_sums_kernel raises it)}
+__global__ __launch_bounds__(kST) void st_bfs_arrays_kernel(const uint32_t* __restrict__ kA, const uint32_t* __restrict__ vA,
+                                                            const uint32_t* __restrict__ kB, const uint32_t* __restrict__ vB,
+                                                            int launched, const uint32_t* __restrict__ chw, int P,
+                                                            int* __restrict__ rank, uint32_t* __restrict__ child,
+                                                            int* __restrict__ lev, int* __restrict__ hdr) {
+    const int i = blockIdx.x * kST + threadIdx.x;
+    if (i >= P) return;
+    const bool inB = st_radix_passes_run(hdr, launched) & 1;
+    const uint32_t* node = inB ? vB : vA;
+    const uint32_t* dep = inB ? kB : kA;
+    const uint32_t p = min(node[i], (uint32_t)P - 1u);
+    rank[p] = i;
+    child[i] = chw[p];
+    const int d = (int)min(dep[i], (uint32_t)P - 1u);
+    if (i == 0 || dep[i - 1] != dep[i]) lev[d] = i;
+    if (i == P - 1) {
+        lev[d + 1] = P;
+        hdr[0] = d + 1;
+        hdr[1] = 1;
+    }
+}
+
+// first = 1 + the exclusive scan of the child counts; node i writes its children's parent index and
+// distance byte (the root's: -1, 0)
+struct StChildCount {
+    const uint32_t* child;
+    __device__ uint32_t operator()(int i) const { return child[i] & 0xFFu; }
+};
+struct StFirstOut {
+    const uint32_t* child;
+    int* first;
+    int* parent;
+    uint8_t* pdist;
+    int P;
+    __device__ void operator()(int i, uint32_t e, uint32_t n) const {
+        const int f = 1 + (int)e;
+        first[i] = f;
+        const uint32_t ch = child[i];
+        for (int z = 0; z < (int)n; ++z) {
+            if (f + z < P) {
+                parent[f + z] = i;
+                pdist[f + z] = (uint8_t)(ch >> (8 * (z + 1)));
+            }
+        }
+        if (i == 0) {
+            parent[0] = -1;
+            pdist[0] = 0;
+        }
+    }
+};
+
+// tasks of <= 64 nodes per level; the sums pass also raises hdr[1] to the widest level
+struct StLevelTasks {
+    const int* lev;
+    const int* hdr;
+    __device__ uint32_t operator()(int l) const { return l < hdr[0] ? (uint32_t)(lev[l + 1] - lev[l] + 63) / 64u : 0u; }
+};
+struct StIntOut {
+    int* out;
+    __device__ void operator()(int i, uint32_t e, uint32_t) const { out[i] = (int)e; }
+};
+__global__ __launch_bounds__(64) void st_level_sums_kernel(const int* __restrict__ lev, int* __restrict__ hdr, int n,
+                                                           uint32_t* __restrict__ sums) {
+    const int lane = threadIdx.x, blk = blockIdx.x, nlev = hdr[0];
+    uint32_t t = 0;
+    int wmax = 1;
+    for (int r = 0; r < kScRounds; ++r) {
+        const int l = blk * kScIPB + r * 64 + lane;
+        if (l < n && l < nlev) {
+            const int w = lev[l + 1] - lev[l];
+            t += (uint32_t)(w + 63) / 64u;
+            wmax = max(wmax, w);
+        }
+    }
+    t = wave_scan_v(t, lane);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off, 64));
+    if (lane == 63) sums[blk] = t;
+    if (lane == 0 && blk * kScIPB < nlev) atomicMax(&hdr[1], wmax);
+}
+
+// wave_tasks on the device: level l's up tasks after those of the levels below it in the up order
+// (levels - 1 .. 0), its down tasks (levels 1 .. levels - 1) after the up list; E = the exclusive scan of
+// the per-level task counts, hdr[2] its total (= the up tasks); writes hdr[3] = the down tasks
+__global__ __launch_bounds__(kST) void st_task_kernel(const int* __restrict__ lev, const int* __restrict__ E,
+                                                      int* __restrict__ hdr, int P, int4* __restrict__ task) {
+    const int l = blockIdx.x * kST + threadIdx.x;
+    const int nlev = hdr[0];
+    if (l >= P || l >= nlev) return;
+    const int stride = hdr[1] + 64, total = hdr[2];
+    const int lo = lev[l], hi = lev[l + 1], q = l & 1, nt = (hi - lo + 63) / 64;
+    auto cut = [&](int4* dst, int other) {
+        const int rb = kStLvlOff + ((q ^ 1) * stride - other) * 4;
+        for (int t = 0; t < nt; ++t) {
+            const int s0 = lo + 64 * t;
+            dst[t] = make_int4(s0, min(64, hi - s0) - 1, kStLvlOff + (q * stride + s0 - lo) * 4, rb);
+        }
+    };
+    cut(task + (total - E[l] - nt), l + 1 < nlev ? lev[l + 1] : lo);
+    if (l >= 1) cut(task + total + E[l] - 1, lev[l - 1]);   // level 0 has one task
+    if (l == 0) hdr[3] = total - 1;
 }
 
 // The sorted edges of one tree into page-locked host slot `slot` of the workspace (asynchronous on s).
@@ -621,20 +1001,20 @@ hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* w
     const int passes = depth ? 4 : 1;
     for (int ps = 0; ps < passes; ++ps) {
         const int shift = 8 * ps;
-        hipLaunchKernelGGL(st_rx_hist_kernel, dim3((unsigned)nb), dim3(64), 0, s, k0, n, shift, hist, nb);
-        hipLaunchKernelGGL(st_rx_scan_rows_kernel, dim3(256), dim3(64), 0, s, hist, nb, bases);
-        hipLaunchKernelGGL(st_rx_scan_bases_kernel, dim3(1), dim3(64), 0, s, bases);
+        hipLaunchKernelGGL(st_rx_hist_kernel<kRxRounds>, dim3((unsigned)nb), dim3(64), 0, s, k0, n, shift, hist, nb, nullptr);
+        hipLaunchKernelGGL(st_rx_scan_rows_kernel, dim3(256), dim3(64), 0, s, hist, nb, bases, nullptr, shift);
+        hipLaunchKernelGGL(st_rx_scan_bases_kernel, dim3(1), dim3(64), 0, s, bases, nullptr, shift);
         if (ps + 1 < passes) {
             hipLaunchKernelGGL((st_rx_scatter_kernel<false, false>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
-                               hist, bases, nb, k1, v1, edges, W);
+                               hist, bases, nb, k1, v1, edges, W, nullptr);
             std::swap(k0, k1);
             std::swap(v0, v1);
         } else if (depth) {
             hipLaunchKernelGGL((st_rx_scatter_kernel<true, true>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
-                               hist, bases, nb, k1, v1, edges, W);
+                               hist, bases, nb, k1, v1, edges, W, nullptr);
         } else {
             hipLaunchKernelGGL((st_rx_scatter_kernel<true, false>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
-                               hist, bases, nb, k1, v1, edges, W);
+                               hist, bases, nb, k1, v1, edges, W, nullptr);
         }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -719,6 +1099,142 @@ hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree*& tp) {
     return hipSuccess;
 }
 
+// ---- the device BFS (st_arc_kernel ..): scratch and launch sequence ----
+// SM_ST_HOST_BFS=1 builds the BFS on the host instead (st_host::bfs_tree, round 3's path), read at every
+// call: the A/B baseline and the reference the GPU test compares the device arrays with
+bool host_bfs_requested() {
+    const char* e = std::getenv("SM_ST_HOST_BFS");
+    return e && e[0] == '1';
+}
+
+struct BfsScratch {
+    int2* arcA;        // 4P {next arc, arcs counted}, ping-pong
+    int2* arcB;
+    U2* tw;            // L = 2 (P - 1) tour weights
+    uint2* adj;        // P neighbour lists
+    U2* usums;         // tour scan block sums
+    int* rev;          // 4P reverse arcs
+    int* tv;           // L
+    int* psl;          // P parent slots
+    int* size;         // P subtree sizes
+    int* offs;         // P preorder offsets
+    uint32_t* chw;     // P child words per pixel
+    uint32_t *kA, *vA, *kB, *vB;   // P each: depth keys and pixels of the radix passes
+    uint32_t* hist;    // 256 (nb + 1)
+    uint32_t* sums;    // nb + 2
+    int* E;            // P + 2
+    int* hdr;          // 8: {levels, widest level, up tasks, down tasks, largest depth}
+};
+
+int64_t rx_blocks(int64_t n) { return (n + kScIPB - 1) / kScIPB; }
+
+// ints of the scratch, carved in this order (8- and 16-B arrays first, at even offsets)
+size_t bfs_scratch_ints(int64_t P) {
+    const int64_t L = 2 * (P - 1), nb = rx_blocks(P), nbL = rx_blocks(L);
+    return (size_t)(8 * P * 2 + 2 * L + 2 * P + 2 * (nbL + 2) + 4 * P + L + 4 * P + 4 * P + 256 * (nb + 1) + (nb + 2) +
+                    (P + 2) + 8);
+}
+
+BfsScratch bfs_scratch(int* base, int64_t P) {
+    const int64_t L = 2 * (P - 1), nb = rx_blocks(P), nbL = rx_blocks(L);
+    BfsScratch b{};
+    int* q = base;
+    auto take = [&](int64_t n) {
+        int* r = q;
+        q += n;
+        return r;
+    };
+    b.arcA = reinterpret_cast<int2*>(take(8 * P));
+    b.arcB = reinterpret_cast<int2*>(take(8 * P));
+    b.tw = reinterpret_cast<U2*>(take(2 * L));
+    b.adj = reinterpret_cast<uint2*>(take(2 * P));
+    b.usums = reinterpret_cast<U2*>(take(2 * (nbL + 2)));
+    b.rev = take(4 * P);
+    b.tv = take(L);
+    b.psl = take(P);
+    b.size = take(P);
+    b.offs = take(P);
+    b.chw = reinterpret_cast<uint32_t*>(take(P));
+    b.kA = reinterpret_cast<uint32_t*>(take(P));
+    b.vA = reinterpret_cast<uint32_t*>(take(P));
+    b.kB = reinterpret_cast<uint32_t*>(take(P));
+    b.vB = reinterpret_cast<uint32_t*>(take(P));
+    b.hist = reinterpret_cast<uint32_t*>(take(256 * (nb + 1)));
+    b.sums = reinterpret_cast<uint32_t*>(take(nb + 2));
+    b.E = take(P + 2);
+    b.hdr = take(8);
+    return b;
+}
+
+// tasks per tree slot: up and down each <= P / 64 + levels, levels <= P
+size_t task_slot_cap(int64_t P) { return (size_t)(2 * (P + P / 64 + 2)); }
+
+int ceil_log2(int64_t n) {
+    int r = 0;
+    while (((int64_t)1 << r) < n) ++r;
+    return r;
+}
+
+// The BFS of the neighbour lists at h_adj (page-locked, P records, consumed once the copy has run) into
+// device tree slot d and the wave filter's tasks into `task` (task_slot_cap(P) int4), all on stream s;
+// the header {levels, widest level, up tasks, down tasks} lands in page-locked h_hdr once the stream has
+// passed the copy this enqueues last.
+hipError_t gpu_bfs(StWorkspace& ws, int scr, const AdjRec* h_adj, int P, int W, const DevTree& d, int4* task, int* h_hdr,
+                   hipStream_t s) {
+    hipError_t e;
+    if ((e = grow(ws.bfs[scr], ws.bfs_n[scr], bfs_scratch_ints(P))) != hipSuccess) return e;
+    const BfsScratch b = bfs_scratch(ws.bfs[scr], P);
+    const int L = 2 * (P - 1), nb = (int)rx_blocks(P), nbL = (int)rx_blocks(L);
+    if ((e = hipMemsetAsync(b.hdr, 0, 8 * sizeof(int), s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(b.adj, h_adj, (size_t)P * sizeof(AdjRec), hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    const dim3 gP((unsigned)((P + kST - 1) / kST)), g4P((unsigned)((4 * (int64_t)P + kST - 1) / kST));
+    // 1. rank the tour: jumps of 2^r cover its L arcs after ceil(log2 L) steps; root it
+    hipLaunchKernelGGL(st_arc_kernel, gP, dim3(kST), 0, s, b.adj, P, W, b.arcA, b.rev);
+    int2 *ain = b.arcA, *aout = b.arcB;
+    for (int r = ceil_log2(L); r > 0; --r) {
+        hipLaunchKernelGGL(st_list_rank_kernel, g4P, dim3(kST), 0, s, ain, aout, 4 * P);
+        std::swap(ain, aout);
+    }
+    hipLaunchKernelGGL(st_root_kernel, gP, dim3(kST), 0, s, b.adj, ain, b.rev, P, b.psl, b.size);
+    // 2. preorder offsets, the tour's prefix sums -> depth and preorder of every node
+    hipLaunchKernelGGL(st_child_kernel, gP, dim3(kST), 0, s, b.adj, b.psl, b.size, P, W, b.offs, b.chw);
+    hipLaunchKernelGGL(st_tour_kernel, gP, dim3(kST), 0, s, b.adj, ain, b.psl, b.offs, P, W, b.tw, b.tv);
+    hipLaunchKernelGGL((st_scan_sums_kernel<U2, StTourW>), dim3((unsigned)nbL), dim3(64), 0, s, StTourW{b.tw}, L, b.usums);
+    hipLaunchKernelGGL(st_scan_rows_kernel<U2>, dim3(1), dim3(64), 0, s, b.usums, nbL, nullptr);
+    hipLaunchKernelGGL(st_tour_apply_kernel, dim3((unsigned)nbL), dim3(64), 0, s, b.tw, b.tv, L, b.usums, b.kA, b.vA, P,
+                       b.hdr);
+    // 3. stable sort by depth (< P): 8-bit digits up to P - 1's top bit, passes above the deepest level's
+    // top bit skipped on the device
+    uint32_t *k0 = b.kA, *v0 = b.vA, *k1 = b.kB, *v1 = b.vB;
+    uint32_t* bases = b.hist + (size_t)256 * nb;
+    int launched = 0;
+    for (int shift = 0; shift < std::max(1, ceil_log2(P)); shift += 8, ++launched) {
+        hipLaunchKernelGGL(st_rx_hist_kernel<kScRounds>, dim3((unsigned)nb), dim3(64), 0, s, k0, P, shift, b.hist, nb, b.hdr);
+        hipLaunchKernelGGL(st_rx_scan_rows_kernel, dim3(256), dim3(64), 0, s, b.hist, nb, bases, b.hdr, shift);
+        hipLaunchKernelGGL(st_rx_scan_bases_kernel, dim3(1), dim3(64), 0, s, bases, b.hdr, shift);
+        hipLaunchKernelGGL((st_rx_scatter_kernel<false, false, kScRounds>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, P,
+                           shift, b.hist, bases, nb, k1, v1, nullptr, W, b.hdr);
+        std::swap(k0, k1);
+        std::swap(v0, v1);
+    }
+    // 4. the BFS-order arrays, first / parent / pdist, the wave filter's tasks
+    hipLaunchKernelGGL(st_bfs_arrays_kernel, gP, dim3(kST), 0, s, b.kA, b.vA, b.kB, b.vB, launched, b.chw, P, d.rank,
+                       d.child, d.lev, b.hdr);
+    const StChildCount cc{d.child};
+    hipLaunchKernelGGL((st_scan_sums_kernel<uint32_t, StChildCount>), dim3((unsigned)nb), dim3(64), 0, s, cc, P, b.sums);
+    hipLaunchKernelGGL(st_scan_rows_kernel<uint32_t>, dim3(1), dim3(64), 0, s, b.sums, nb, nullptr);
+    hipLaunchKernelGGL((st_scan_apply_kernel<uint32_t, StChildCount, StFirstOut>), dim3((unsigned)nb), dim3(64), 0, s, cc,
+                       P, b.sums, StFirstOut{d.child, d.first, d.parent, d.pdist, P});
+    hipLaunchKernelGGL(st_level_sums_kernel, dim3((unsigned)nb), dim3(64), 0, s, d.lev, b.hdr, P, b.sums);
+    hipLaunchKernelGGL(st_scan_rows_kernel<uint32_t>, dim3(1), dim3(64), 0, s, b.sums, nb,
+                       reinterpret_cast<uint32_t*>(b.hdr + 2));
+    hipLaunchKernelGGL((st_scan_apply_kernel<uint32_t, StLevelTasks, StIntOut>), dim3((unsigned)nb), dim3(64), 0, s,
+                       StLevelTasks{d.lev, b.hdr}, P, b.sums, StIntOut{b.E});
+    hipLaunchKernelGGL(st_task_kernel, gP, dim3(kST), 0, s, d.lev, b.E, b.hdr, P, task);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return hipMemcpyAsync(h_hdr, b.hdr, 4 * sizeof(int), hipMemcpyDeviceToHost, s);
+}
+
 // A tree bound by host_tree_slot: its level offsets join the ints, which go up as one copy (rank .. lev),
 // then pdist and the weight table.  `t`'s slot and `table` must stay alive until the stream has consumed
 // the copies.
@@ -732,6 +1248,14 @@ hipError_t upload_tree(const HostTree& t, const float* table, int64_t P, DevTree
         return e;
     if ((e = hipMemcpyAsync(d.pdist, t.pdist, (size_t)P, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     return hipMemcpyAsync(d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s);
+}
+
+// WTA of the filtered cost F (BFS order) of tree d into the map `out` (pixel order); node: P ints of scratch
+hipError_t launch_wta(const float* F, const DevTree& d, int* node, int P, int D, int scale, uint8_t* out, hipStream_t s) {
+    const dim3 g((unsigned)((P + kST - 1) / kST));
+    hipLaunchKernelGGL(st_node_kernel, g, dim3(kST), 0, s, d.rank, P, node);
+    hipLaunchKernelGGL(st_wta_kernel, g, dim3(kST), 0, s, F, node, P, D, scale, out);
+    return hipGetLastError();
 }
 
 FilterJob filter_job(float* C, float* F, const DevTree& d) {
@@ -767,18 +1291,6 @@ int wave_tasks(const HostTree& t, std::vector<int4>& out, int& n_up, int& n_dn) 
 
 constexpr int kWaveMaxLevel = (65536 - kStLvlOff) / 8 - 64;   // 64 KB of LDS; wider trees keep st_filter_kernel
 
-// Host task list `tv` of tree `d` into task slot k (`per` int4 each) of the workspace, which the caller
-// has grown for all its slots before the first upload; tv must stay alive until the copy has run.
-hipError_t upload_wave_job(StWorkspace& ws, int k, size_t per, const std::vector<int4>& tv, float* C, float* F,
-                           const DevTree& d, int n_up, int n_dn, hipStream_t s, WaveJob& j) {
-    if (tv.size() > per || ws.task_n < per * 4 * (size_t)(k + 1)) return hipErrorInvalidValue;
-    int4* dst = reinterpret_cast<int4*>(ws.task) + per * (size_t)k;
-    const hipError_t e = hipMemcpyAsync(dst, tv.data(), tv.size() * sizeof(int4), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
-    j = WaveJob{C, F, d.parent, d.pdist, d.first, d.child, dst, n_up, n_dn, d.table};
-    return hipSuccess;
-}
-
 // One filter launch over 1 or 2 jobs: the wave filter when every level fits its LDS buffers, else the
 // workgroup-per-disparity filter.
 // SM_ST_WAVE_FILTER=0 forces the workgroup filter (the path of trees wider than the wave filter's LDS,
@@ -801,6 +1313,92 @@ hipError_t launch_filter(const FilterJobs& fj, const WaveJobs& wj, int njobs, in
     return hipGetLastError();
 }
 
+// A built tree's filter inputs: its device slot, its tasks and their counts
+struct TreeJob {
+    DevTree d;
+    int4* task;
+    int maxw, n_up, n_dn;
+};
+
+// Neighbour-list storage of tree slot k: page-locked (the slot's h_tree, (5P + 2) * 4 + P >= 8P bytes) for
+// the device BFS; the tree's own vector for the host BFS, whose arrays take the page-locked slot
+AdjRec* list_storage(StWorkspace& ws, HostTree& t, int k, bool hbfs, int64_t P) {
+    if (hbfs) {
+        t.adj.resize((size_t)P);
+        return t.adj.data();
+    }
+    return static_cast<AdjRec*>(ws.h_tree[k]);
+}
+
+// The host part of one tree from the sorted edges of edge slot `slot`: segment_graph's passes into the
+// lists, starting on the first downloaded chunk, and with hbfs the BFS too.  False on a failed build.
+bool host_tree_part(StWorkspace& ws, int slot, HostTree& t, AdjRec* adj, bool hbfs, int nE, int64_t P, int W, float tau,
+                    float wscale) {
+    bool arrived = true;
+    segment_lists(static_cast<Edge*>(ws.h_edges[slot]), nE, (int)P, tau, wscale, t, ws.edge_chunk[slot],
+                  [&](int upto) { arrived = arrived && wait_edges(ws, slot, upto); }, adj);
+    if (!arrived) return false;
+    return !hbfs || bfs_tree(adj, (int)P, W, t);
+}
+
+// Enqueue tree slot k's device part: the weight table and the device BFS (header to h_hdr + 4 k, scratch
+// ws.bfs[k]), or with hbfs the host tree's upload and its host tasks (`tv` must stay alive until the stream
+// has run the copy).  The caller grows ws.task to task_slot_cap(P) per slot first.
+hipError_t enqueue_tree(StWorkspace& ws, HostTree& t, const AdjRec* adj, bool hbfs, int64_t P, int W, const float* table,
+                        int k, hipStream_t s, std::vector<int4>& tv, TreeJob& j) {
+    j.d = tree_slot(ws, P, k);
+    j.task = reinterpret_cast<int4*>(ws.task) + task_slot_cap(P) * (size_t)k;
+    hipError_t e;
+    if (!ws.h_hdr) return hipErrorNotInitialized;   // tree_resources
+    if (!hbfs) {
+        if ((e = hipMemcpyAsync(j.d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s)) != hipSuccess)
+            return e;
+        return gpu_bfs(ws, k, adj, (int)P, W, j.d, j.task, ws.h_hdr + 4 * k, s);
+    }
+    if ((e = upload_tree(t, table, P, j.d, s)) != hipSuccess) return e;
+    j.maxw = wave_tasks(t, tv, j.n_up, j.n_dn);
+    if (tv.size() > task_slot_cap(P)) return hipErrorInvalidValue;
+    return hipMemcpyAsync(j.task, tv.data(), tv.size() * sizeof(int4), hipMemcpyHostToDevice, s);
+}
+
+// Per-call resources of the tree builds, allocated before any build thread starts: task slots for `trees`
+// trees, the page-locked headers, the events and (two trees) the side stream
+hipError_t tree_resources(StWorkspace& ws, int64_t P, int trees) {
+    hipError_t e;
+    if ((e = grow(ws.task, ws.task_n, task_slot_cap(P) * 4 * (size_t)trees)) != hipSuccess) return e;
+    if (!ws.h_hdr && (e = hipHostMalloc(&ws.h_hdr, 8 * sizeof(int), hipHostMallocDefault)) != hipSuccess) return e;
+    if (!ws.bfs_ev && (e = hipEventCreateWithFlags(&ws.bfs_ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (trees > 1) {
+        if (!ws.side_ev && (e = hipEventCreateWithFlags(&ws.side_ev, hipEventDisableTiming)) != hipSuccess) return e;
+        if (!ws.side && (e = hipStreamCreateWithFlags(&ws.side, hipStreamNonBlocking)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// After the enqueue_tree calls: an event behind the device BFS's header copies (work enqueued after it,
+// e.g. the cost volume, runs while read_trees waits)
+hipError_t mark_trees(StWorkspace& ws, hipStream_t s) { return hipEventRecord(ws.bfs_ev, s); }
+
+// The device BFS's headers of tree slots [0, n) once mark_trees' event has passed (host BFS: known already)
+hipError_t read_trees(StWorkspace& ws, bool hbfs, TreeJob* j, int n, int64_t P) {
+    if (hbfs) return hipSuccess;
+    const hipError_t e = hipEventSynchronize(ws.bfs_ev);
+    if (e != hipSuccess) return e;
+    for (int k = 0; k < n; ++k) {
+        const int* h = ws.h_hdr + 4 * k;
+        if (h[0] < 1 || h[0] > P || h[1] < 1 || h[1] > P || h[2] < 1 || h[3] != h[2] - 1) return hipErrorUnknown;
+        j[k].d.nlev = h[0];
+        j[k].maxw = h[1];
+        j[k].n_up = h[2];
+        j[k].n_dn = h[3];
+    }
+    return hipSuccess;
+}
+
+WaveJob wave_job(float* C, float* F, const TreeJob& t) {
+    return WaveJob{C, F, t.d.parent, t.d.pdist, t.d.first, t.d.child, t.task, t.n_up, t.n_dn, t.d.table};
+}
+
 float ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -818,9 +1416,26 @@ void StWorkspace::release() {
     (void)hipFree(table);
     (void)hipFree(task);
     task = nullptr;
+    (void)hipFree(node);
+    node = nullptr;
+    node_n = 0;
     (void)hipFree(sortbuf);
     sortbuf = nullptr;
     sortbuf_n = 0;
+    for (int k = 0; k < 2; ++k) {
+        (void)hipFree(bfs[k]);
+        bfs[k] = nullptr;
+        bfs_n[k] = 0;
+    }
+    if (side) (void)hipStreamDestroy(side);
+    side = nullptr;
+    if (side_ev) (void)hipEventDestroy(side_ev);
+    side_ev = nullptr;
+    if (h_hdr) (void)hipHostFree(h_hdr);
+    h_hdr = nullptr;
+    if (bfs_ev) (void)hipEventDestroy(bfs_ev);
+    bfs_ev = nullptr;
+    last_P = last_nlev = 0;
     for (int k = 0; k < 2; ++k) {
         if (h_edges[k]) (void)hipHostFree(h_edges[k]);
         h_edges[k] = nullptr;
@@ -861,6 +1476,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     ST_CHK(grow(ws.tree_i, ws.tree_i_n, (size_t)P * 5 + 2));
     ST_CHK(grow(ws.tree_b, ws.tree_b_n, (size_t)P));
     ST_CHK(grow(ws.table, ws.table_n, (size_t)256));
+    ST_CHK(grow(ws.node, ws.node_n, (size_t)P));
     const dim3 rows((unsigned)((W + kST - 1) / kST), (unsigned)H);
     // guide weights -> host
     uint8_t* wr = ws.w8;
@@ -874,47 +1490,47 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
     ST_CHK(hipGetLastError());
-    // tree on the host, into page-locked memory, starting on the first edge chunk (no stream sync: the
-    // gradients run meanwhile)
+    // segment_graph's passes on the host, starting on the first edge chunk (no stream sync: the gradients
+    // run meanwhile), into page-locked lists; the BFS on the device
     const auto t0 = std::chrono::steady_clock::now();
+    const bool hbfs = host_bfs_requested();
     HostTree* tp = nullptr;
     ST_CHK(host_tree_slot(ws, P, 0, tp));
     HostTree& t = *tp;
-    bool arrived = true;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 1.0f, t, ws.edge_chunk[0],
-                         [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
-        !arrived) {
+    AdjRec* adj = list_storage(ws, t, 0, hbfs, P);
+    if (!host_tree_part(ws, 0, t, adj, hbfs, nE, P, W, tau, 1.0f)) {
         (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
     }
     float table[256];
     weight_table(sigma, table);
-    const float tree_ms = ms_since(t0);
-    DevTree dt = tree_slot(ws, P, 0);
-    ST_CHK(upload_tree(t, table, P, dt, s));
+    ST_CHK(tree_resources(ws, P, 1));
     std::vector<int4> tv;
-    int n_up = 0, n_dn = 0;
-    const int maxw = wave_tasks(t, tv, n_up, n_dn);
-    ST_CHK(grow(ws.task, ws.task_n, tv.size() * 4));
+    TreeJob tj{};
+    ST_CHK(enqueue_tree(ws, t, adj, hbfs, P, W, table, 0, s, tv, tj));
+    ST_CHK(mark_trees(ws, s));
+    const DevTree& dt = tj.d;
     float* C = ws.vol;
     float* F = ws.vol + (size_t)P * D;
-    WaveJobs wj{};
-    ST_CHK(upload_wave_job(ws, 0, tv.size(), tv, C, F, dt, n_up, n_dn, s, wj.j[0]));
     hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
                        dt.rank, D, C);
     ST_CHK(hipGetLastError());
+    ST_CHK(read_trees(ws, hbfs, &tj, 1, P));
+    const float tree_ms = ms_since(t0);
     FilterJobs jobs{};
-    jobs.j[0] = filter_job(C, F, dt);
-    ST_CHK(launch_filter(jobs, wj, 1, maxw, D, (int)P, s));
+    jobs.j[0] = filter_job(C, F, tj.d);
+    WaveJobs wj{};
+    wj.j[0] = wave_job(C, F, tj);
+    ST_CHK(launch_filter(jobs, wj, 1, tj.maxw, D, (int)P, s));
     uint8_t* raw = ws.w8;   // the weights are consumed: reuse for the unfiltered map
-    hipLaunchKernelGGL(st_wta_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, F, dt.rank, (int)P, D,
-                       scale, raw);
-    ST_CHK(hipGetLastError());
+    ST_CHK(launch_wta(F, dt, ws.node, (int)P, D, scale, raw, s));
     ST_CHK(launch_median(raw, W, H, W, P, 1, 3, d_out, W, P, s));   // MeanFilter(disparity, disparity, 3)
     if (st) {
-        st->levels = dt.nlev;
+        st->levels = tj.d.nlev;
         st->tree_ms = tree_ms;
     }
+    ws.last_P = (int)P;
+    ws.last_nlev = tj.d.nlev;
     // keep the host tree alive until its uploads have been consumed
     return hipStreamSynchronize(s);
 }
@@ -932,8 +1548,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(grow(ws.tree_i, ws.tree_i_n, ((size_t)P * 5 + 2) * 2));
     ST_CHK(grow(ws.tree_b, ws.tree_b_n, (size_t)P * 2));
     ST_CHK(grow(ws.table, ws.table_n, (size_t)512));
+    ST_CHK(grow(ws.node, ws.node_n, (size_t)P * 2));
     const dim3 rows((unsigned)((W + kST - 1) / kST), (unsigned)H);
-    const dim3 pix((unsigned)((P + kST - 1) / kST));
     uint8_t* wrL = ws.w8;
     uint8_t* wrR = ws.w8 + 2 * P;
     uint8_t* raw0 = ws.w8 + 4 * P;
@@ -953,40 +1569,62 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dL, W, H, pitch, ws.grad);
     hipLaunchKernelGGL(st_gradient_kernel, rows, dim3(kST), 0, s, dR, W, H, pitch, ws.grad + P);
     ST_CHK(hipGetLastError());
-    // first run: colour trees of the left and the right view, built side by side (StereoDisparity.cpp:112-123)
-    // into page-locked slots 0 and 1, each starting on the first chunk of its edges
+    // first run: colour trees of the left and the right view, segment_graph's passes side by side
+    // (StereoDisparity.cpp:112-123) into page-locked lists 0 and 1, each starting on the first chunk of its
+    // edges; each build enqueues its BFS as soon as its lists are done, the left on s, the right on the
+    // side stream (the two BFSs are chains of small latency-bound kernels: side by side they overlap)
     auto t0 = std::chrono::steady_clock::now();
+    const bool hbfs = host_bfs_requested();
+    ST_CHK(tree_resources(ws, P, 2));
     HostTree *tlp = nullptr, *trp = nullptr;
     ST_CHK(host_tree_slot(ws, P, 0, tlp));
     ST_CHK(host_tree_slot(ws, P, 1, trp));
     HostTree &tl = *tlp, &tr = *trp;
+    AdjRec* adjL = list_storage(ws, tl, 0, hbfs, P);
+    AdjRec* adjR = list_storage(ws, tr, 1, hbfs, P);
+    float tab1[256];
+    weight_table(kSigmaOne, tab1);
+    std::vector<int4> tv[2];
+    TreeJob tj[2] = {};
+    hipStream_t bs[2] = {s, ws.side};
     // neither build may leave its exception behind the other's thread (a joinable std::thread must not
-    // be destroyed): a failed build reports false
-    auto build = [&](int slot, HostTree& t) {
+    // be destroyed): a failed build reports false, a failed enqueue its error
+    auto build = [&](int slot, HostTree& t, AdjRec* adj, hipError_t& err) {
         try {
-            bool arrived = true;
-            const bool ok = tree_from_edges(static_cast<Edge*>(ws.h_edges[slot]), nE, (int)P, W, tau, 1.0f, t,
-                                            ws.edge_chunk[slot],
-                                            [&](int upto) { arrived = arrived && wait_edges(ws, slot, upto); });
-            return ok && arrived;
+            if (!host_tree_part(ws, slot, t, adj, hbfs, nE, P, W, tau, 1.0f)) return false;
+            if (!hbfs) {
+                err = enqueue_tree(ws, t, adj, false, P, W, tab1, slot, bs[slot], tv[slot], tj[slot]);
+                if (err == hipSuccess && slot == 1) err = hipEventRecord(ws.side_ev, ws.side);
+            }
+            return true;
         } catch (...) {
             return false;
         }
     };
     bool okR = false;
-    std::thread th([&] { okR = build(1, tr); });
-    const bool okL = build(0, tl);
+    hipError_t errL = hipSuccess, errR = hipSuccess;
+    int dev = 0;
+    ST_CHK(hipGetDevice(&dev));
+    std::thread th([&] {
+        errR = hipSetDevice(dev);   // the current device is per thread (the scratch allocation, the launches)
+        if (errR == hipSuccess) okR = build(1, tr, adjR, errR);
+    });
+    const bool okL = build(0, tl, adjL, errL);
     th.join();
-    if (!okL || !okR) {
-        (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
-        return hipErrorInvalidValue;
+    if (!okL || !okR || errL != hipSuccess || errR != hipSuccess) {
+        // no copy into the page-locked buffers may outlive the call
+        (void)hipStreamSynchronize(ws.side);
+        (void)hipStreamSynchronize(s);
+        return errL != hipSuccess ? errL : errR != hipSuccess ? errR : hipErrorInvalidValue;
     }
-    float tab1[256];
-    weight_table(kSigmaOne, tab1);
-    float tree_ms = ms_since(t0);
-    DevTree d0 = tree_slot(ws, P, 0), d1 = tree_slot(ws, P, 1);
-    ST_CHK(upload_tree(tl, tab1, P, d0, s));
-    ST_CHK(upload_tree(tr, tab1, P, d1, s));
+    if (hbfs) {
+        ST_CHK(enqueue_tree(ws, tl, adjL, true, P, W, tab1, 0, s, tv[0], tj[0]));
+        ST_CHK(enqueue_tree(ws, tr, adjR, true, P, W, tab1, 1, s, tv[1], tj[1]));
+    } else {
+        ST_CHK(hipStreamWaitEvent(s, ws.side_ev, 0));
+    }
+    ST_CHK(mark_trees(ws, s));
+    const DevTree &d0 = tj[0].d, &d1 = tj[1].d;
     float* C0 = ws.vol;
     float* F0 = ws.vol + (size_t)P * D;
     float* C1 = ws.vol + (size_t)P * D * 2;
@@ -996,21 +1634,17 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     hipLaunchKernelGGL(st_cost_kernel<true>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
                        d1.rank, D, C1);
     ST_CHK(hipGetLastError());
+    ST_CHK(read_trees(ws, hbfs, tj, 2, P));
+    float tree_ms = ms_since(t0);
     FilterJobs jobs{};
     jobs.j[0] = filter_job(C0, F0, d0);
     jobs.j[1] = filter_job(C1, F1, d1);
-    std::vector<int4> tv0, tv1;
-    int nu0 = 0, nd0 = 0, nu1 = 0, nd1 = 0;
-    const int mw0 = wave_tasks(tl, tv0, nu0, nd0), mw1 = wave_tasks(tr, tv1, nu1, nd1);
-    const size_t per = std::max(tv0.size(), tv1.size());
-    ST_CHK(grow(ws.task, ws.task_n, per * 4 * 2));
     WaveJobs wj{};
-    ST_CHK(upload_wave_job(ws, 0, per, tv0, C0, F0, d0, nu0, nd0, s, wj.j[0]));
-    ST_CHK(upload_wave_job(ws, 1, per, tv1, C1, F1, d1, nu1, nd1, s, wj.j[1]));
-    ST_CHK(launch_filter(jobs, wj, 2, std::max(mw0, mw1), D, (int)P, s));
-    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, 1, raw0);
-    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F1, d1.rank, (int)P, D, 1, raw1);
-    ST_CHK(hipGetLastError());
+    wj.j[0] = wave_job(C0, F0, tj[0]);
+    wj.j[1] = wave_job(C1, F1, tj[1]);
+    ST_CHK(launch_filter(jobs, wj, 2, std::max(tj[0].maxw, tj[1].maxw), D, (int)P, s));
+    ST_CHK(launch_wta(F0, d0, ws.node, (int)P, D, 1, raw0, s));
+    ST_CHK(launch_wta(F1, d1, ws.node + P, (int)P, D, 1, raw1, s));
     ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, mapL, W, P, s));   // MeanFilter(disparityLeft, ..., 3)
     ST_CHK(launch_median(raw1, W, H, W, P, 1, 3, mapR, W, P, s));
     // left-right check (StereoDisparity.cpp:129-147): mask = !occluded
@@ -1025,40 +1659,39 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
         return hipErrorUnknown;
     }
     t0 = std::chrono::steady_clock::now();
-    HostTree* tdp = nullptr;   // slot 0's tree object again: the left tree's tasks are uploaded
+    HostTree* tdp = nullptr;   // slot 0's tree object again
     ST_CHK(host_tree_slot(ws, P, 0, tdp));
     HostTree& td = *tdp;
-    bool arrived = true;
-    if (!tree_from_edges(static_cast<Edge*>(ws.h_edges[0]), nE, (int)P, W, tau, 255.0f, td, ws.edge_chunk[0],
-                         [&](int upto) { arrived = arrived && wait_edges(ws, 0, upto); }) ||
-        !arrived) {
+    AdjRec* adjD = list_storage(ws, td, 0, hbfs, P);
+    if (!host_tree_part(ws, 0, td, adjD, hbfs, nE, P, W, tau, 255.0f)) {
         (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
     }
     float tab2[256];
     weight_table(sigma, tab2);
-    tree_ms += ms_since(t0);
-    ST_CHK(upload_tree(td, tab2, P, d0, s));
+    std::vector<int4> tv2;
+    TreeJob t2{};
+    ST_CHK(enqueue_tree(ws, td, adjD, hbfs, P, W, tab2, 0, s, tv2, t2));
+    ST_CHK(mark_trees(ws, s));
     // second run on the same cost (the reference recomputes it, :150)
     hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
-                       d0.rank, D, C0);
+                       t2.d.rank, D, C0);
     ST_CHK(hipGetLastError());
+    ST_CHK(read_trees(ws, hbfs, &t2, 1, P));
+    tree_ms += ms_since(t0);
     FilterJobs job2{};
-    job2.j[0] = filter_job(C0, F0, d0);
-    std::vector<int4> tv2;
-    int nu2 = 0, nd2 = 0;
-    const int mw2 = wave_tasks(td, tv2, nu2, nd2);
-    ST_CHK(grow(ws.task, ws.task_n, tv2.size() * 4));   // the first run's uploads completed at the sync above
+    job2.j[0] = filter_job(C0, F0, t2.d);
     WaveJobs wj2{};
-    ST_CHK(upload_wave_job(ws, 0, tv2.size(), tv2, C0, F0, d0, nu2, nd2, s, wj2.j[0]));
-    ST_CHK(launch_filter(job2, wj2, 1, mw2, D, (int)P, s));
-    hipLaunchKernelGGL(st_wta_kernel, pix, dim3(kST), 0, s, F0, d0.rank, (int)P, D, scale, raw0);
-    ST_CHK(hipGetLastError());
+    wj2.j[0] = wave_job(C0, F0, t2);
+    ST_CHK(launch_filter(job2, wj2, 1, t2.maxw, D, (int)P, s));
+    ST_CHK(launch_wta(F0, t2.d, ws.node, (int)P, D, scale, raw0, s));
     ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, d_out, W, P, s));
     if (st) {
-        st->levels = d0.nlev;
+        st->levels = t2.d.nlev;
         st->tree_ms = tree_ms;
     }
+    ws.last_P = (int)P;
+    ws.last_nlev = t2.d.nlev;
     return hipStreamSynchronize(s);
 }
 

@@ -93,7 +93,7 @@ void each_edge(int W, int P, F&& f) {
 
 // CColorWeight edges (integer weights) in edge::operator< order (SegmentTree.h:103-111): a counting sort
 // by weight filled in (b, a) order is that order exactly.
-std::vector<Edge> sorted_edges_u8(const uint8_t* wr, const uint8_t* wu, int W, int P) {
+inline std::vector<Edge> sorted_edges_u8(const uint8_t* wr, const uint8_t* wu, int W, int P) {
     std::vector<int> cnt(257, 0);
     each_edge(W, P, [&](int a, int, int up) { cnt[(up ? wu[a] : wr[a]) + 1]++; });
     for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
@@ -107,7 +107,7 @@ std::vector<Edge> sorted_edges_u8(const uint8_t* wr, const uint8_t* wu, int W, i
 
 // Float-weighted edges (CColorDepthWeight) in edge::operator< order: generated in (b, a) order, then a
 // stable LSD radix sort on the weights' bit patterns (non-negative floats order as their bits).
-std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P) {
+inline std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P) {
     std::vector<Edge> e, tmp;
     e.reserve((size_t)2 * P);
     each_edge(W, P, [&](int a, int b, int up) { e.push_back(Edge{a, b, up ? wu[a] : wr[a]}); });
@@ -134,10 +134,13 @@ std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W, int P)
 // lists are 8 B per pixel (four distances, four 2-bit directions, the count) instead of 24.
 // `arrived(i)` (round 4) returns once edges [0, i) are readable: the GPU path downloads the sorted edges in
 // chunks and the first pass starts on the first chunk while the rest is still in flight.  It is called
-// with increasing i at most every `step` edges, and with nE before the second pass.  The tree's arrays
-// must be bound (HostTree::bind) unless it owns none yet.
+// with increasing i at most every `step` edges, and with nE before the second pass.
+// Split in two (round 4): segment_lists (segment_graph's two passes into the neighbour lists `adj`, P
+// records) and bfs_tree (the BFS from the lists); the GPU path runs the first here and the BFS on the
+// device (bm_segtree.hip, st_arc_kernel ..), into the same arrays.
 template <class Arrived>
-bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step, Arrived&& arrived) {
+void segment_lists(Edge* e, int nE, int P, float tau, float wscale, HostTree& t, int step, Arrived&& arrived,
+                   AdjRec* adj) {
 SM_ST_NO_CONTRACT
     // segment_graph (segment-graph.h:48-101) on disjoint-set.h's forest (Dsu's rules, roots packed)
     std::vector<int>& par = t.par;
@@ -180,8 +183,7 @@ SM_ST_NO_CONTRACT
     }
     SM_ST_PHASE(0);
     // neighbour lists (AdjRec)
-    std::vector<AdjRec>& adj = t.adj;
-    adj.assign(P, AdjRec{0u, 0, 0});
+    std::fill(adj, adj + P, AdjRec{0u, 0, 0});
     auto link = [&](int pa, int pb, uint8_t dis) {
         const int diff = pb - pa;
         const uint32_t da = diff == -1 ? 0u : diff == 1 ? 1u : diff < 0 ? 2u : 3u;
@@ -206,8 +208,12 @@ SM_ST_NO_CONTRACT
         link(e[i].a, e[i].b, (uint8_t)std::min((int)(sw + 0.5f), 255));
     }
     SM_ST_PHASE(1);
-    // BFS from pixel 0 (SegmentTree.cpp:97-130), level by level; every entry is written once the tree
-    // spans the image (end == P), so the arrays need no clearing beyond the root's
+}
+
+// BFS from pixel 0 (SegmentTree.cpp:97-130) over the neighbour lists, level by level; every entry is
+// written once the tree spans the image (end == P), so the arrays need no clearing beyond the root's.
+// The tree's arrays must be bound (HostTree::bind) unless it owns none yet.
+inline bool bfs_tree(const AdjRec* adj, int P, int W, HostTree& t) {
     const int off[4] = {-1, 1, -W, W};
     if (!t.rank) t.bind(P);
     t.node.resize(P);
@@ -255,19 +261,26 @@ SM_ST_NO_CONTRACT
     return end == P;
 }
 
+template <class Arrived>
+bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step, Arrived&& arrived) {
+    t.adj.resize(P);
+    segment_lists(e, nE, P, tau, wscale, t, step, arrived, t.adj.data());
+    return bfs_tree(t.adj.data(), P, W, t);
+}
+
 // every edge already in memory
-bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
+inline bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
     return tree_from_edges(e, nE, P, W, tau, wscale, t, nE, [](int) {});
 }
 
-bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
+inline bool build_tree(const uint8_t* wr, const uint8_t* wu, int W, int H, float tau, HostTree& t) {
     std::vector<Edge> e = sorted_edges_u8(wr, wu, W, W * H);
     return tree_from_edges(e.data(), (int)e.size(), W * H, W, tau, 1.0f, t);
 }
 
 // CColorDepthWeight::GetWeight (SegmentTree.cpp:204-219) from the colour weights (max channel |diff| on
 // the 3x3-median guide), the first left map and the mask, in the reference's float operations
-void depth_weights(const uint8_t* wr, const uint8_t* wu, const uint8_t* disp, const uint8_t* mask, int W, int H,
+inline void depth_weights(const uint8_t* wr, const uint8_t* wu, const uint8_t* disp, const uint8_t* mask, int W, int H,
                    float level, float* fr, float* fu) {
 SM_ST_NO_CONTRACT
     auto weight = [&](int p, int q, uint8_t c) -> float {

@@ -1488,6 +1488,22 @@ SM_API int sm_last_segment_tree_stats(sm_handle* h, float* tree_ms, float* total
     return SM_OK;
 }
 
+SM_API int sm_last_segment_tree_arrays(sm_handle* h, int* ints, int64_t n_ints, uint8_t* pdist, int64_t n_bytes,
+                                       int* levels) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!h->st_valid || h->st.last_P <= 0) return fail(SM_ERR_INVALID_ARG, "no segment-tree call has completed on this handle");
+    const int64_t P = h->st.last_P, nlev = h->st.last_nlev, need = 4 * P + nlev + 1;
+    if (!ints || !pdist || n_ints < need || n_bytes < P)
+        return fail(SM_ERR_INVALID_ARG, "buffers too small: %lld ints and %lld bytes needed", (long long)need,
+                    (long long)P);
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(hipStreamSynchronize(h->stream));
+    SM_HIP(hipMemcpy(ints, h->st.tree_i, (size_t)need * sizeof(int), hipMemcpyDeviceToHost));
+    SM_HIP(hipMemcpy(pdist, h->st.tree_b, (size_t)P, hipMemcpyDeviceToHost));
+    if (levels) *levels = (int)nlev;
+    return SM_OK;
+}
+
 SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const uint8_t* right_bgr, int width,
                                  int height, int pitch, int channels, int radius, int num_disp, unsigned flags,
                                  uint8_t* disp_out, int out_pitch) {

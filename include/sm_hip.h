@@ -262,14 +262,21 @@ SM_API int sm_segment_tree_match_bgr_u8(sm_handle *h, const uint8_t *left_bgr, c
  * of each view (sigma SIGMA_ONE = 0.08, Toolkit.h:35; the right cost taken from the left's,
  * StereoHelper.cpp:156-180), each WTA + 7x7 median; the left-right check (:129-147); then a colour +
  * depth tree (CColorDepthWeight, SegmentTree.cpp:196-219) on the left view, the first left map and
- * the check's mask, filtered with `sigma`, WTA, 7x7 median, x scale.  The three trees are built on the
- * host (the first two on two threads); everything O(P*D) runs on the GPU.  Synchronous. */
+ * the check's mask, filtered with `sigma`, WTA, 7x7 median, x scale.  The three trees' segment_graph
+ * passes run on the host (the first two on two threads), their BFS on the GPU; everything O(P*D) runs
+ * on the GPU.  Synchronous. */
 SM_API int sm_segment_tree_refined_bgr_u8(sm_handle *h, const uint8_t *left_bgr, const uint8_t *right_bgr,
                                           int width, int height, int pitch, int max_level, int scale, float sigma,
                                           uint8_t *disp_out, int out_pitch);
-/* last segment-tree call (either method): host tree-build time, whole-call time (ms) and the last tree's
- * BFS level count */
+/* last segment-tree call (either method): tree-build time (the host's segment_graph passes and the BFS,
+ * until its level count is known), whole-call time (ms) and the last tree's BFS level count */
 SM_API int sm_last_segment_tree_stats(sm_handle *h, float *tree_ms, float *total_ms, int *levels);
+/* diagnostics: the last call's last tree (ST-1 its colour tree, ST-2 the colour + depth tree) in BFS
+ * order, as SegmentTree.cpp:97-130 lays it out: ints = rank[P] (pixel -> BFS index), parent[P],
+ * first[P] (first child), child[P] (count | distance bytes << 8), level offsets[levels + 1]
+ * (n_ints >= 4P + levels + 1); pdist[P] = distance byte to the parent.  Synchronous. */
+SM_API int sm_last_segment_tree_arrays(sm_handle *h, int *ints, int64_t n_ints, uint8_t *pdist, int64_t n_bytes,
+                                       int *levels);
 
 /* ---- several GPUs from one host thread (sm_create_group) ----
  * A group holds one handle and one host worker thread per device (devices == NULL: 0..ngpu-1;

@@ -131,3 +131,39 @@ def test_workgroup_filter_fallback():
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "OK" in out.stdout, out.stdout
+
+
+def _bfs_cases():
+    g = np.load(os.path.join(GOLDEN, "middlebury_bgr.npz"))
+    yield "art", g["Art/view1"], g["Art/view5"], 60
+    for W, H, seed in ((97, 61, 31), (2, 5, 32), (123, 1, 33)):
+        rng = np.random.default_rng(seed)
+        L = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        L[: H // 2, : W // 3] = 77
+        yield f"{W}x{H}", L, np.roll(L, -min(5, W - 1), axis=1), 16
+    flat = np.full((40, 30, 3), 9, np.uint8)                 # every weight equal: a comb-shaped tree
+    yield "flat", flat, flat, 8
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_device_bfs_equals_host_bfs(matcher, method):
+    """The BFS on the GPU (Euler tour + pointer jumping + depth sort, bm_segtree.hip) against the host's
+    BFS (st_host::bfs_tree, SM_ST_HOST_BFS=1, itself checked against oracle/st_oracle.c by
+    tests/test_st_host.py): the tree arrays the filter reads (rank, parent, first, child words, level
+    offsets, parent distances) identical, for ST-1's colour tree and ST-2's colour + depth tree, and the
+    maps identical."""
+    for name, L, R, D in _bfs_cases():
+        H, W, _ = L.shape
+        os.environ["SM_ST_HOST_BFS"] = "1"
+        try:
+            want_map = matcher.segment_tree(L, R, D, 2, 0.1, method=method)
+            want = matcher.segment_tree_arrays(W, H)
+        finally:
+            del os.environ["SM_ST_HOST_BFS"]
+        got_map = matcher.segment_tree(L, R, D, 2, 0.1, method=method)
+        got = matcher.segment_tree_arrays(W, H)
+        assert len(got["lev"]) == len(want["lev"]), name
+        for k in want:
+            assert np.array_equal(got[k], want[k]), (name, k, int((got[k] != want[k]).sum()))
+        assert np.array_equal(got_map, want_map), name
+        assert matcher.segment_tree_stats()[2] == len(want["lev"]) - 1
