@@ -314,11 +314,12 @@ def run_variants(sm, torch, dev, stream, seed):
                 "ms_per_frame": round(ms, 4), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1}
             del Lp, Rp, Op, pair
         # STMatching's segment-tree stereo, ST-1 and ST-2 (§8f rank 4), on the bundled Art pair at the app's
-        # defaults: a synchronous host call (host tree builds + GPU cost / filter / WTA / median / LR check), wall
+        # defaults: a synchronous host call (host segment_graph passes + GPU BFS / cost / filter / WTA / median /
+        # LR check), wall
         g = np.load(os.path.join(ROOT, "tests", "golden", "middlebury_bgr.npz"))
         Lb, Rb = g["Art/view1"], g["Art/view5"]
-        for method, label in ((0, "segment tree ST-1 Art 463x370 d60 (host tree + GPU filter, wall)"),
-                              (1, "segment tree ST-2 Art 463x370 d60 (3 host trees + GPU filters + LR check, wall)")):
+        for method, label in ((0, "segment tree ST-1 Art 463x370 d60 (host segmentation + GPU BFS and filter, wall)"),
+                              (1, "segment tree ST-2 Art 463x370 d60 (3 trees: host segmentation + GPU BFS, filters, LR check, wall)")):
             for _ in range(2):
                 m.segment_tree(Lb, Rb, method=method)
             ts = []
@@ -329,7 +330,7 @@ def run_variants(sm, torch, dev, stream, seed):
             tree_ms, _, levels = m.segment_tree_stats()
             ms = float(np.median(ts))
             out[label] = {"ms_per_frame": round(ms, 3), "maps_per_s": round(1000.0 / ms, 1), "frames_per_call": 1,
-                          "host_tree_ms": round(tree_ms, 3), "tree_levels": levels}
+                          "tree_ms": round(tree_ms, 3), "tree_levels": levels}
     finally:
         m.close()
     return out
