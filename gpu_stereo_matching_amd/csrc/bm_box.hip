@@ -638,6 +638,21 @@ bool wide_tiles_enabled() {
     return on;
 }
 
+// Launches of more tiles than CUs but at most SM_BOX_MID_MAX (default 8) tiles per CU (batch 1 of a
+// mid-size frame) take 8-wave tiles, the d pairs split over twice the waves: the last round of tiles
+// ends sooner.  Same box, device resident, batch 1 (profiles/microbench/r04_box_mid_tiles_latency.txt):
+// 960x540 D=128 47.5 -> 39.7 us, 320x240 D=32 16.7 -> 13.6, 1080p D=128 88.5 -> 86.3; maps identical.
+// SM_BOX_MID=0 (read once) keeps the 4-wave tiles (A/B).
+int mid_tiles_max() {
+    static const int v = [] {
+        const char* e = std::getenv("SM_BOX_MID");
+        if (e && e[0] == '0') return 0;
+        const char* m = std::getenv("SM_BOX_MID_MAX");
+        return m ? std::atoi(m) : 8;
+    }();
+    return v;
+}
+
 template <int R, int DMAX, bool RIGHT>
 hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStream_t s) {
     using G = Geo<R, DMAX, kWavesD<RIGHT, R, DMAX>>;
@@ -675,6 +690,14 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
                 using GW = Geo<R, DMAX, kWideTile>;
                 hipLaunchKernelGGL((box_match_kernel<R, DMAX, false, kWideTile>), dim3((unsigned)blocks),
                                    dim3(64 * kWideTile), (size_t)GW::LDS_BYTES, s, a, tiles_x, tiles_y);
+                return hipGetLastError();
+            }
+        }
+        if constexpr (!kWideR<R>) {
+            if (mid_tiles_max() > 0 && blocks <= (int64_t)mid_tiles_max() * compute_units() && npairs >= 16) {
+                using GM = Geo<R, DMAX, 8>;
+                hipLaunchKernelGGL((box_match_kernel<R, DMAX, false, 8>), dim3((unsigned)blocks), dim3(64 * 8),
+                                   (size_t)GM::LDS_BYTES, s, a, tiles_x, tiles_y);
                 return hipGetLastError();
             }
         }
