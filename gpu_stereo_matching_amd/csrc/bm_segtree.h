@@ -26,6 +26,12 @@ struct StWorkspace {
     int last_P = 0, last_nlev = 0; // tree slot 0 of the last call (sm_last_segment_tree_arrays)
     uint32_t* sortbuf = nullptr;   // edge sort: keys and values (2 x 2 nE), digit counts, sorted edges (3 nE)
     void* h_edges[2] = {nullptr, nullptr};   // page-locked host copies of sorted edges (12 B each), 2 trees
+    // round 4, per edge slot: the sorted edges on the device (12 B each) and each grid edge's sorted
+    // position (2P); the host passes' per-edge marks, page-locked (nE bytes)
+    uint32_t* dedge[2] = {nullptr, nullptr};
+    int* sidx[2] = {nullptr, nullptr};
+    void* h_marks[2] = {nullptr, nullptr};
+    size_t dedge_n[2] = {0, 0}, sidx_n[2] = {0, 0}, h_marks_n[2] = {0, 0};
     // page-locked host trees (round 4), one per tree slot: ints in the device slot's layout (rank, parent,
     // first, child: 4P; level offsets: P + 2), then pdist (P bytes): one DMA copy per tree
     void* h_tree[2] = {nullptr, nullptr};

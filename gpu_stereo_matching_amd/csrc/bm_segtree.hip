@@ -554,7 +554,8 @@ __global__ __launch_bounds__(64) void st_rx_scatter_kernel(const uint32_t* __res
                                                            int n, int shift, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ bases, int nb,
                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                           st_host::Edge* __restrict__ eout, int W, const int* gate) {
+                                                           st_host::Edge* __restrict__ eout, int W, const int* gate,
+                                                           int* __restrict__ sidx = nullptr) {
     if (st_rx_skip(gate, shift)) return;
     __shared__ uint32_t cnt[256];
     const int lane = threadIdx.x, blk = blockIdx.x;
@@ -584,6 +585,7 @@ __global__ __launch_bounds__(64) void st_rx_scatter_kernel(const uint32_t* __res
                 const int b = (int)(v >> 1);
                 eout[pos] = st_host::Edge{(v & 1u) ? b + W : b - 1, b,
                                           DEPTH ? __builtin_bit_cast(float, k) : (float)k};
+                sidx[v] = (int)pos;   // grid edge v's sorted position (st_adj_kernel)
             } else {
                 kout[pos] = k;
                 vout[pos] = v;
@@ -620,6 +622,62 @@ static_assert(sizeof(st_host::AdjRec) == 8, "AdjRec is read as a uint2 {d, dir |
 __device__ __forceinline__ int st_nb(int p, uint32_t dir, int k, int W) {
     const uint32_t c = (dir >> (2 * k)) & 3u;
     return c == 0 ? p - 1 : c == 1 ? p + 1 : c == 2 ? p - W : p + W;
+}
+
+// The neighbour lists from the host passes' marks (segment_passes): pixel p's tree edges in sorted-edge
+// order, as segment_lists appends them (SegmentTree.cpp:74-95), each with its direction code (0: p - 1,
+// 1: p + 1, 2: p - W, 3: p + W) and distance min(int(w' * wscale + 0.5), 255), w' = w (+ 5 when
+// penalised, st_host::tree_dist).  Grid edge v = 2 b + (edge is (b + W, b)) sits at sorted position
+// sidx[v].  Out: AdjRec bits {d, dir | n << 16}.
+__global__ __launch_bounds__(kST) void st_adj_kernel(const st_host::Edge* __restrict__ edges, const int* __restrict__ sidx,
+                                                     const uint8_t* __restrict__ marks, int W, int P, float wscale,
+                                                     uint2* __restrict__ adj) {
+#pragma clang fp contract(off)
+    const int p = blockIdx.x * kST + threadIdx.x;
+    if (p >= P) return;
+    const int x = p % W;
+    int pos[4];
+    uint32_t cd[4];   // direction code | distance << 8
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const bool ex = c == 0 ? x >= 1 : c == 1 ? x + 1 < W : c == 2 ? p >= W : p + W < P;
+        const int v = c == 0 ? 2 * p : c == 1 ? 2 * (p + 1) : c == 2 ? 2 * (p - W) + 1 : 2 * p + 1;
+        pos[c] = INT_MAX;
+        cd[c] = 0;
+        if (ex) {
+            const int q = sidx[v];
+            const uint8_t m = marks[q];
+            if (m & 1u) {
+                float w = edges[q].w;
+                if (m & 2u) w += 5;
+                const float sw = w * wscale;
+                pos[c] = q;
+                cd[c] = (uint32_t)c | ((uint32_t)min((int)(sw + 0.5f), 255) << 8);
+            }
+        }
+    }
+    // sort the (at most 4) tree edges by sorted position
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j > 0; --j)
+            if (pos[j] < pos[j - 1]) {
+                const int tp = pos[j];
+                pos[j] = pos[j - 1];
+                pos[j - 1] = tp;
+                const uint32_t tc = cd[j];
+                cd[j] = cd[j - 1];
+                cd[j - 1] = tc;
+            }
+    uint32_t d = 0, dir = 0, n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (pos[k] != INT_MAX) {
+            d |= (cd[k] >> 8) << (8 * k);
+            dir |= (cd[k] & 3u) << (2 * k);
+            ++n;
+        }
+    adj[p] = make_uint2(d, dir | (n << 16));
 }
 
 // arcs: slot k of pixel p is arc 4 p + k {next arc of the tour, 1}; the arc into arc 0 (pixel 0 to its
@@ -974,10 +1032,12 @@ hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* w
     const int64_t n64 = st_edge_count(W, H);
     if (n64 <= 0 || n64 > (1 << 30)) return hipErrorInvalidValue;
     const int n = (int)n64, nb = (n + kRxIPB - 1) / kRxIPB;
-    // keys / values x 2, digit counts, edge records (3 dwords each)
-    const size_t need = (size_t)4 * n + (size_t)256 * (nb + 1) + (size_t)3 * n;
+    // keys / values x 2, digit counts; the edge records (3 dwords each) and sorted positions per slot
+    const size_t need = (size_t)4 * n + (size_t)256 * (nb + 1);
     hipError_t e;
     if ((e = grow(ws.sortbuf, ws.sortbuf_n, need)) != hipSuccess) return e;
+    if ((e = grow(ws.dedge[slot], ws.dedge_n[slot], (size_t)3 * n)) != hipSuccess) return e;
+    if ((e = grow(ws.sidx[slot], ws.sidx_n[slot], (size_t)2 * W * H)) != hipSuccess) return e;
     const size_t hbytes = (size_t)n * sizeof(st_host::Edge);
     if (ws.h_edges_n[slot] < hbytes) {
         if (ws.h_edges[slot]) (void)hipHostFree(ws.h_edges[slot]);
@@ -992,7 +1052,8 @@ hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* w
     uint32_t* v1 = k1 + n;
     uint32_t* hist = v1 + n;
     uint32_t* bases = hist + (size_t)256 * nb;
-    auto* edges = reinterpret_cast<st_host::Edge*>(bases + 256);
+    auto* edges = reinterpret_cast<st_host::Edge*>(ws.dedge[slot]);
+    int* sidx = ws.sidx[slot];
     const dim3 rows((unsigned)((W + kST - 1) / kST), (unsigned)H);
     if (depth)
         hipLaunchKernelGGL(st_edge_keys_kernel<true>, rows, dim3(kST), 0, s, wr, wu, disp, mask, level, W, H, k0, v0);
@@ -1011,10 +1072,10 @@ hipError_t gpu_sorted_edges(StWorkspace& ws, const uint8_t* wr, const uint8_t* w
             std::swap(v0, v1);
         } else if (depth) {
             hipLaunchKernelGGL((st_rx_scatter_kernel<true, true>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
-                               hist, bases, nb, k1, v1, edges, W, nullptr);
+                               hist, bases, nb, k1, v1, edges, W, nullptr, sidx);
         } else {
             hipLaunchKernelGGL((st_rx_scatter_kernel<true, false>), dim3((unsigned)nb), dim3(64), 0, s, k0, v0, n, shift,
-                               hist, bases, nb, k1, v1, edges, W, nullptr);
+                               hist, bases, nb, k1, v1, edges, W, nullptr, sidx);
         }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1081,9 +1142,10 @@ void weight_table(float sigma, float* table) {
 
 // Page-locked host tree of slot k (StWorkspace::h_tree): ints (5P + 2) in the device slot's layout, then
 // pdist (P bytes); the slot's previous upload must have completed before a new tree is bound to it.
-hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree*& tp) {
+hipError_t host_tree_slot(StWorkspace& ws, int64_t P, int k, HostTree*& tp, bool hbfs = true) {
     if (!ws.host_tree[k]) ws.host_tree[k] = new HostTree();
     tp = static_cast<HostTree*>(ws.host_tree[k]);
+    if (!hbfs) return hipSuccess;   // the device BFS: the host keeps only the passes' forest
     HostTree& t = *tp;
     const size_t need = (size_t)(5 * P + 2) * 4 + (size_t)P;
     if (ws.h_tree_n[k] < need) {
@@ -1124,18 +1186,19 @@ struct BfsScratch {
     uint32_t* sums;    // nb + 2
     int* E;            // P + 2
     int* hdr;          // 8: {levels, widest level, up tasks, down tasks, largest depth}
+    uint8_t* marks;    // nE: the host passes' marks
 };
 
 int64_t rx_blocks(int64_t n) { return (n + kScIPB - 1) / kScIPB; }
 
 // ints of the scratch, carved in this order (8- and 16-B arrays first, at even offsets)
-size_t bfs_scratch_ints(int64_t P) {
+size_t bfs_scratch_ints(int64_t P, int64_t nE) {
     const int64_t L = 2 * (P - 1), nb = rx_blocks(P), nbL = rx_blocks(L);
     return (size_t)(8 * P * 2 + 2 * L + 2 * P + 2 * (nbL + 2) + 4 * P + L + 4 * P + 4 * P + 256 * (nb + 1) + (nb + 2) +
-                    (P + 2) + 8);
+                    (P + 2) + 8 + (nE + 3) / 4);
 }
 
-BfsScratch bfs_scratch(int* base, int64_t P) {
+BfsScratch bfs_scratch(int* base, int64_t P, int64_t nE) {
     const int64_t L = 2 * (P - 1), nb = rx_blocks(P), nbL = rx_blocks(L);
     BfsScratch b{};
     int* q = base;
@@ -1163,6 +1226,7 @@ BfsScratch bfs_scratch(int* base, int64_t P) {
     b.sums = reinterpret_cast<uint32_t*>(take(nb + 2));
     b.E = take(P + 2);
     b.hdr = take(8);
+    b.marks = reinterpret_cast<uint8_t*>(take((nE + 3) / 4));
     return b;
 }
 
@@ -1175,19 +1239,23 @@ int ceil_log2(int64_t n) {
     return r;
 }
 
-// The BFS of the neighbour lists at h_adj (page-locked, P records, consumed once the copy has run) into
+// The neighbour lists and their BFS from edge slot scr's marks (ws.h_marks[scr], page-locked, nE bytes,
+// consumed once the copy has run) and sorted edges (ws.dedge / ws.sidx[scr], from gpu_sorted_edges) into
 // device tree slot d and the wave filter's tasks into `task` (task_slot_cap(P) int4), all on stream s;
 // the header {levels, widest level, up tasks, down tasks} lands in page-locked h_hdr once the stream has
 // passed the copy this enqueues last.
-hipError_t gpu_bfs(StWorkspace& ws, int scr, const AdjRec* h_adj, int P, int W, const DevTree& d, int4* task, int* h_hdr,
-                   hipStream_t s) {
+hipError_t gpu_bfs(StWorkspace& ws, int scr, int P, int W, int nE, float wscale, const DevTree& d, int4* task,
+                   int* h_hdr, hipStream_t s) {
     hipError_t e;
-    if ((e = grow(ws.bfs[scr], ws.bfs_n[scr], bfs_scratch_ints(P))) != hipSuccess) return e;
-    const BfsScratch b = bfs_scratch(ws.bfs[scr], P);
+    if ((e = grow(ws.bfs[scr], ws.bfs_n[scr], bfs_scratch_ints(P, nE))) != hipSuccess) return e;
+    const BfsScratch b = bfs_scratch(ws.bfs[scr], P, nE);
     const int L = 2 * (P - 1), nb = (int)rx_blocks(P), nbL = (int)rx_blocks(L);
     if ((e = hipMemsetAsync(b.hdr, 0, 8 * sizeof(int), s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(b.adj, h_adj, (size_t)P * sizeof(AdjRec), hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(b.marks, ws.h_marks[scr], (size_t)nE, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     const dim3 gP((unsigned)((P + kST - 1) / kST)), g4P((unsigned)((4 * (int64_t)P + kST - 1) / kST));
+    // 0. the neighbour lists from the marks and the edge slot's sorted edges
+    hipLaunchKernelGGL(st_adj_kernel, gP, dim3(kST), 0, s, reinterpret_cast<const st_host::Edge*>(ws.dedge[scr]),
+                       ws.sidx[scr], b.marks, W, P, wscale, b.adj);
     // 1. rank the tour: jumps of 2^r cover its L arcs after ceil(log2 L) steps; root it
     hipLaunchKernelGGL(st_arc_kernel, gP, dim3(kST), 0, s, b.adj, P, W, b.arcA, b.rev);
     int2 *ain = b.arcA, *aout = b.arcB;
@@ -1320,32 +1388,38 @@ struct TreeJob {
     int maxw, n_up, n_dn;
 };
 
-// Neighbour-list storage of tree slot k: page-locked (the slot's h_tree, (5P + 2) * 4 + P >= 8P bytes) for
-// the device BFS; the tree's own vector for the host BFS, whose arrays take the page-locked slot
+// Neighbour-list storage of the host BFS path (the tree's own vector; its arrays take the page-locked
+// slot); the device path builds the lists on the GPU (null)
 AdjRec* list_storage(StWorkspace& ws, HostTree& t, int k, bool hbfs, int64_t P) {
-    if (hbfs) {
-        t.adj.resize((size_t)P);
-        return t.adj.data();
-    }
-    return static_cast<AdjRec*>(ws.h_tree[k]);
+    (void)ws;
+    (void)k;
+    if (!hbfs) return nullptr;
+    t.adj.resize((size_t)P);
+    return t.adj.data();
 }
 
-// The host part of one tree from the sorted edges of edge slot `slot`: segment_graph's passes into the
-// lists, starting on the first downloaded chunk, and with hbfs the BFS too.  False on a failed build.
+// The host part of one tree from the sorted edges of edge slot `slot`: segment_graph's passes, starting
+// on the first downloaded chunk, into the slot's page-locked marks; with hbfs the neighbour lists and
+// the BFS on the host instead.  False on a failed build.
 bool host_tree_part(StWorkspace& ws, int slot, HostTree& t, AdjRec* adj, bool hbfs, int nE, int64_t P, int W, float tau,
                     float wscale) {
     bool arrived = true;
-    segment_lists(static_cast<Edge*>(ws.h_edges[slot]), nE, (int)P, tau, wscale, t, ws.edge_chunk[slot],
-                  [&](int upto) { arrived = arrived && wait_edges(ws, slot, upto); }, adj);
-    if (!arrived) return false;
-    return !hbfs || bfs_tree(adj, (int)P, W, t);
+    auto hook = [&](int upto) { arrived = arrived && wait_edges(ws, slot, upto); };
+    const Edge* e = static_cast<const Edge*>(ws.h_edges[slot]);
+    if (hbfs) {
+        segment_lists(e, nE, (int)P, tau, wscale, t, ws.edge_chunk[slot], hook, adj);
+        return arrived && bfs_tree(adj, (int)P, W, t);
+    }
+    segment_passes(e, nE, (int)P, tau, t, ws.edge_chunk[slot], hook, static_cast<uint8_t*>(ws.h_marks[slot]),
+                   [](int) {});
+    return arrived;
 }
 
 // Enqueue tree slot k's device part: the weight table and the device BFS (header to h_hdr + 4 k, scratch
 // ws.bfs[k]), or with hbfs the host tree's upload and its host tasks (`tv` must stay alive until the stream
 // has run the copy).  The caller grows ws.task to task_slot_cap(P) per slot first.
-hipError_t enqueue_tree(StWorkspace& ws, HostTree& t, const AdjRec* adj, bool hbfs, int64_t P, int W, const float* table,
-                        int k, hipStream_t s, std::vector<int4>& tv, TreeJob& j) {
+hipError_t enqueue_tree(StWorkspace& ws, HostTree& t, bool hbfs, int64_t P, int W, int nE, float wscale,
+                        const float* table, int k, hipStream_t s, std::vector<int4>& tv, TreeJob& j) {
     j.d = tree_slot(ws, P, k);
     j.task = reinterpret_cast<int4*>(ws.task) + task_slot_cap(P) * (size_t)k;
     hipError_t e;
@@ -1353,7 +1427,7 @@ hipError_t enqueue_tree(StWorkspace& ws, HostTree& t, const AdjRec* adj, bool hb
     if (!hbfs) {
         if ((e = hipMemcpyAsync(j.d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s)) != hipSuccess)
             return e;
-        return gpu_bfs(ws, k, adj, (int)P, W, j.d, j.task, ws.h_hdr + 4 * k, s);
+        return gpu_bfs(ws, k, (int)P, W, nE, wscale, j.d, j.task, ws.h_hdr + 4 * k, s);
     }
     if ((e = upload_tree(t, table, P, j.d, s)) != hipSuccess) return e;
     j.maxw = wave_tasks(t, tv, j.n_up, j.n_dn);
@@ -1363,9 +1437,17 @@ hipError_t enqueue_tree(StWorkspace& ws, HostTree& t, const AdjRec* adj, bool hb
 
 // Per-call resources of the tree builds, allocated before any build thread starts: task slots for `trees`
 // trees, the page-locked headers, the events and (two trees) the side stream
-hipError_t tree_resources(StWorkspace& ws, int64_t P, int trees) {
+hipError_t tree_resources(StWorkspace& ws, int64_t P, int nE, int trees) {
     hipError_t e;
     if ((e = grow(ws.task, ws.task_n, task_slot_cap(P) * 4 * (size_t)trees)) != hipSuccess) return e;
+    for (int k = 0; k < trees; ++k) {
+        if (ws.h_marks_n[k] >= (size_t)nE) continue;
+        if (ws.h_marks[k]) (void)hipHostFree(ws.h_marks[k]);
+        ws.h_marks[k] = nullptr;
+        ws.h_marks_n[k] = 0;
+        if ((e = hipHostMalloc(&ws.h_marks[k], (size_t)nE, hipHostMallocDefault)) != hipSuccess) return e;
+        ws.h_marks_n[k] = (size_t)nE;
+    }
     if (!ws.h_hdr && (e = hipHostMalloc(&ws.h_hdr, 8 * sizeof(int), hipHostMallocDefault)) != hipSuccess) return e;
     if (!ws.bfs_ev && (e = hipEventCreateWithFlags(&ws.bfs_ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (trees > 1) {
@@ -1443,6 +1525,15 @@ void StWorkspace::release() {
         if (h_tree[k]) (void)hipHostFree(h_tree[k]);
         h_tree[k] = nullptr;
         h_tree_n[k] = 0;
+        if (h_marks[k]) (void)hipHostFree(h_marks[k]);
+        h_marks[k] = nullptr;
+        h_marks_n[k] = 0;
+        (void)hipFree(dedge[k]);
+        dedge[k] = nullptr;
+        dedge_n[k] = 0;
+        (void)hipFree(sidx[k]);
+        sidx[k] = nullptr;
+        sidx_n[k] = 0;
         delete static_cast<st_host::HostTree*>(host_tree[k]);
         host_tree[k] = nullptr;
         for (auto& ev : edge_ev[k]) {
@@ -1494,8 +1585,9 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     // run meanwhile), into page-locked lists; the BFS on the device
     const auto t0 = std::chrono::steady_clock::now();
     const bool hbfs = host_bfs_requested();
+    ST_CHK(tree_resources(ws, P, nE, 1));
     HostTree* tp = nullptr;
-    ST_CHK(host_tree_slot(ws, P, 0, tp));
+    ST_CHK(host_tree_slot(ws, P, 0, tp, hbfs));
     HostTree& t = *tp;
     AdjRec* adj = list_storage(ws, t, 0, hbfs, P);
     if (!host_tree_part(ws, 0, t, adj, hbfs, nE, P, W, tau, 1.0f)) {
@@ -1504,10 +1596,9 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     }
     float table[256];
     weight_table(sigma, table);
-    ST_CHK(tree_resources(ws, P, 1));
     std::vector<int4> tv;
     TreeJob tj{};
-    ST_CHK(enqueue_tree(ws, t, adj, hbfs, P, W, table, 0, s, tv, tj));
+    ST_CHK(enqueue_tree(ws, t, hbfs, P, W, nE, 1.0f, table, 0, s, tv, tj));
     ST_CHK(mark_trees(ws, s));
     const DevTree& dt = tj.d;
     float* C = ws.vol;
@@ -1575,10 +1666,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     // side stream (the two BFSs are chains of small latency-bound kernels: side by side they overlap)
     auto t0 = std::chrono::steady_clock::now();
     const bool hbfs = host_bfs_requested();
-    ST_CHK(tree_resources(ws, P, 2));
+    ST_CHK(tree_resources(ws, P, nE, 2));
     HostTree *tlp = nullptr, *trp = nullptr;
-    ST_CHK(host_tree_slot(ws, P, 0, tlp));
-    ST_CHK(host_tree_slot(ws, P, 1, trp));
+    ST_CHK(host_tree_slot(ws, P, 0, tlp, hbfs));
+    ST_CHK(host_tree_slot(ws, P, 1, trp, hbfs));
     HostTree &tl = *tlp, &tr = *trp;
     AdjRec* adjL = list_storage(ws, tl, 0, hbfs, P);
     AdjRec* adjR = list_storage(ws, tr, 1, hbfs, P);
@@ -1593,7 +1684,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
         try {
             if (!host_tree_part(ws, slot, t, adj, hbfs, nE, P, W, tau, 1.0f)) return false;
             if (!hbfs) {
-                err = enqueue_tree(ws, t, adj, false, P, W, tab1, slot, bs[slot], tv[slot], tj[slot]);
+                err = enqueue_tree(ws, t, false, P, W, nE, 1.0f, tab1, slot, bs[slot], tv[slot], tj[slot]);
                 if (err == hipSuccess && slot == 1) err = hipEventRecord(ws.side_ev, ws.side);
             }
             return true;
@@ -1618,8 +1709,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
         return errL != hipSuccess ? errL : errR != hipSuccess ? errR : hipErrorInvalidValue;
     }
     if (hbfs) {
-        ST_CHK(enqueue_tree(ws, tl, adjL, true, P, W, tab1, 0, s, tv[0], tj[0]));
-        ST_CHK(enqueue_tree(ws, tr, adjR, true, P, W, tab1, 1, s, tv[1], tj[1]));
+        ST_CHK(enqueue_tree(ws, tl, true, P, W, nE, 1.0f, tab1, 0, s, tv[0], tj[0]));
+        ST_CHK(enqueue_tree(ws, tr, true, P, W, nE, 1.0f, tab1, 1, s, tv[1], tj[1]));
     } else {
         ST_CHK(hipStreamWaitEvent(s, ws.side_ev, 0));
     }
@@ -1660,7 +1751,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     }
     t0 = std::chrono::steady_clock::now();
     HostTree* tdp = nullptr;   // slot 0's tree object again
-    ST_CHK(host_tree_slot(ws, P, 0, tdp));
+    ST_CHK(host_tree_slot(ws, P, 0, tdp, hbfs));
     HostTree& td = *tdp;
     AdjRec* adjD = list_storage(ws, td, 0, hbfs, P);
     if (!host_tree_part(ws, 0, td, adjD, hbfs, nE, P, W, tau, 255.0f)) {
@@ -1671,7 +1762,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     weight_table(sigma, tab2);
     std::vector<int4> tv2;
     TreeJob t2{};
-    ST_CHK(enqueue_tree(ws, td, adjD, hbfs, P, W, tab2, 0, s, tv2, t2));
+    ST_CHK(enqueue_tree(ws, td, hbfs, P, W, nE, 255.0f, tab2, 0, s, tv2, t2));
     ST_CHK(mark_trees(ws, s));
     // second run on the same cost (the reference recomputes it, :150)
     hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,

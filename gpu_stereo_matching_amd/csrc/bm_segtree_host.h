@@ -123,24 +123,28 @@ inline std::vector<Edge> sorted_edges_f(const float* wr, const float* wu, int W,
     return e;
 }
 
-// BuildSegmentTree (SegmentTree.cpp:38-139) from the nE sorted edges e (consumed: the cross-segment
-// penalty is added in place) of a W-wide image: segment_graph, the neighbour lists with
-// dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255 colour + depth), BFS from
-// pixel 0, level by level.
+// BuildSegmentTree (SegmentTree.cpp:38-139) from the nE sorted edges e of a W-wide image: segment_graph,
+// the neighbour lists with dist = min(int(w * wscale + 0.5), 255) (wscale = GetScale(): 1 colour, 255
+// colour + depth; w + PENALTY_CROSS_SEG for the penalised edges), BFS from pixel 0, level by level.
 // Round 4 (same trees bit for bit, tests/test_st_host.py): a root's size, rank and threshold in one
 // record (they are read together at every join); the second segment_graph pass skips the edges the
-// first one joined (their ends already share a root) and appends each marked edge to the neighbour
-// lists as it goes, which is the sorted-edge order of SegmentTree.cpp:74-95 without a third pass; the
-// lists are 8 B per pixel (four distances, four 2-bit directions, the count) instead of 24.
+// first one joined (their ends already share a root) and hands each tree edge over as it goes, in the
+// sorted-edge order of SegmentTree.cpp:74-95, without a third pass; the lists are 8 B per pixel (four
+// distances, four 2-bit directions, the count) instead of 24.
 // `arrived(i)` (round 4) returns once edges [0, i) are readable: the GPU path downloads the sorted edges in
 // chunks and the first pass starts on the first chunk while the rest is still in flight.  It is called
 // with increasing i at most every `step` edges, and with nE before the second pass.
-// Split in two (round 4): segment_lists (segment_graph's two passes into the neighbour lists `adj`, P
-// records) and bfs_tree (the BFS from the lists); the GPU path runs the first here and the BFS on the
-// device (bm_segtree.hip, st_arc_kernel ..), into the same arrays.
-template <class Arrived>
-void segment_lists(Edge* e, int nE, int P, float tau, float wscale, HostTree& t, int step, Arrived&& arrived,
-                   AdjRec* adj) {
+// In parts (round 4): segment_passes (segment_graph's two passes: per-edge marks), segment_lists (the
+// passes + the neighbour lists, P records) and bfs_tree (the BFS from the lists).  The GPU path runs
+// only segment_passes here; the lists and the BFS are built on the device from the marks
+// (bm_segtree.hip: st_adj_kernel, st_arc_kernel ..), into the same arrays.
+// segment_graph's two passes over the sorted edges.  marks (nE bytes, written): bit 0 = edge i is a tree
+// edge (joined in either pass), bit 1 = the second pass joined it across two segments both larger than
+// MIN_SIZE_SEG (the PENALTY_CROSS_SEG of +5 on its weight).  on_tree(i) is called for every tree edge in
+// sorted order during the second pass, after its marks are set.
+template <class Arrived, class OnTree>
+void segment_passes(const Edge* e, int nE, int P, float tau, HostTree& t, int step, Arrived&& arrived,
+                    uint8_t* marks, OnTree&& on_tree) {
 SM_ST_NO_CONTRACT
     // segment_graph (segment-graph.h:48-101) on disjoint-set.h's forest (Dsu's rules, roots packed)
     std::vector<int>& par = t.par;
@@ -166,8 +170,7 @@ SM_ST_NO_CONTRACT
         if (R[x].rank == R[y].rank) R[y].rank++;
         return y;
     };
-    std::vector<uint8_t>& mask = t.mask;
-    mask.assign(nE, 0);
+    std::fill(marks, marks + nE, (uint8_t)0);
     int avail = 0;
     for (int i = 0; i < nE; ++i) {
         if (i == avail) {
@@ -176,13 +179,37 @@ SM_ST_NO_CONTRACT
         }
         const int a = find(e[i].a), b = find(e[i].b);
         if (a != b && e[i].w <= R[a].thr && e[i].w <= R[b].thr) {
-            mask[i] = 1;
+            marks[i] = 1;
             const int r = join(a, b);
             R[r].thr = e[i].w + tau / R[r].size;
         }
     }
     SM_ST_PHASE(0);
-    // neighbour lists (AdjRec)
+    for (int i = 0; i < nE; ++i) {
+        if (!marks[i]) {   // segment-graph.h:88-99: join the remaining components
+            const int a = find(e[i].a), b = find(e[i].b);
+            if (a == b) continue;
+            const int size_min = std::min(R[a].size, R[b].size);
+            join(a, b);
+            marks[i] = size_min > 50 ? 3 : 1;   // MIN_SIZE_SEG, PENALTY_CROSS_SEG
+        }
+        on_tree(i);
+    }
+}
+
+// the tree distance of a marked edge: dist = min(int(w * wscale + 0.5), 255) on its (penalised) weight
+inline uint8_t tree_dist(float w, uint8_t mark, float wscale) {
+SM_ST_NO_CONTRACT
+    if (mark & 2) w += 5;
+    const float sw = w * wscale;
+    return (uint8_t)std::min((int)(sw + 0.5f), 255);
+}
+
+// The passes with the neighbour lists built as they go (the host BFS path); `adj` (P records) receives
+// the lists.
+template <class Arrived>
+void segment_lists(const Edge* e, int nE, int P, float tau, float wscale, HostTree& t, int step, Arrived&& arrived,
+                   AdjRec* adj) {
     std::fill(adj, adj + P, AdjRec{0u, 0, 0});
     auto link = [&](int pa, int pb, uint8_t dis) {
         const int diff = pb - pa;
@@ -196,17 +223,10 @@ SM_ST_NO_CONTRACT
         B.dir |= (uint16_t)((da ^ 1u) << (2 * B.n));
         B.n++;
     };
-    for (int i = 0; i < nE; ++i) {
-        if (!mask[i]) {   // segment-graph.h:88-99: join the remaining components
-            const int a = find(e[i].a), b = find(e[i].b);
-            if (a == b) continue;
-            const int size_min = std::min(R[a].size, R[b].size);
-            join(a, b);
-            if (size_min > 50) e[i].w += 5;   // MIN_SIZE_SEG, PENALTY_CROSS_SEG
-        }
-        const float sw = e[i].w * wscale;
-        link(e[i].a, e[i].b, (uint8_t)std::min((int)(sw + 0.5f), 255));
-    }
+    t.mask.resize(nE);
+    uint8_t* marks = t.mask.data();
+    segment_passes(e, nE, P, tau, t, step, arrived, marks,
+                   [&](int i) { link(e[i].a, e[i].b, tree_dist(e[i].w, marks[i], wscale)); });
     SM_ST_PHASE(1);
 }
 
@@ -262,14 +282,15 @@ inline bool bfs_tree(const AdjRec* adj, int P, int W, HostTree& t) {
 }
 
 template <class Arrived>
-bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step, Arrived&& arrived) {
+bool tree_from_edges(const Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t, int step,
+                     Arrived&& arrived) {
     t.adj.resize(P);
     segment_lists(e, nE, P, tau, wscale, t, step, arrived, t.adj.data());
     return bfs_tree(t.adj.data(), P, W, t);
 }
 
 // every edge already in memory
-inline bool tree_from_edges(Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
+inline bool tree_from_edges(const Edge* e, int nE, int P, int W, float tau, float wscale, HostTree& t) {
     return tree_from_edges(e, nE, P, W, tau, wscale, t, nE, [](int) {});
 }
 

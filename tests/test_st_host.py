@@ -25,6 +25,8 @@ def shim(tmp_path_factory):
     L.st_host_tree_u8.argtypes = [u8, u8, ctypes.c_int, ctypes.c_int, ctypes.c_float, i32, i32, u8]
     L.st_host_tree_depth.argtypes = [u8, u8, u8, u8, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                      i32, i32, u8]
+    L.st_host_lists_from_marks_check.argtypes = [u8, u8, u8, u8, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_float]
     return L
 
 
@@ -93,3 +95,19 @@ def test_depth_tree_matches_oracle(oracle, shim, seed, H, W, level):
     assert lv == t["levels"]
     assert np.array_equal(node, t["node"]) and np.array_equal(parent, t["parent"])
     assert np.array_equal(pdist, t["pdist"])
+
+
+@pytest.mark.parametrize("seed,H,W", [(1, 40, 57), (2, 1, 33), (3, 23, 2), (4, 64, 90)])
+@pytest.mark.parametrize("depth", [0, 1])
+def test_lists_from_marks(oracle, shim, seed, H, W, depth):
+    """The device path's neighbour lists (st_adj_kernel) restated on segment_passes' per-edge marks:
+    identical to the lists segment_lists appends during the second pass, for the colour tree and the
+    colour + depth tree (float weights, penalty bit, scale 255)."""
+    L = images(seed, H, W)
+    wr, wu = colour_weights(oracle, L)
+    rng = np.random.default_rng(seed)
+    d = rng.integers(0, 60, (H, W), dtype=np.uint8)
+    m = (rng.random((H, W)) < 0.7).astype(np.uint8)
+    bad = shim.st_host_lists_from_marks_check(_p(wr, ctypes.c_uint8), _p(wu, ctypes.c_uint8), _p(d, ctypes.c_uint8),
+                                              _p(m, ctypes.c_uint8), W, H, 60, depth, 1200.0)
+    assert bad == 0
