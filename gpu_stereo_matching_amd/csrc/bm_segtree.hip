@@ -8,10 +8,12 @@
 //   edge order            GPU: the edges in (b, a) order, stably radix-sorted by weight, which is
 //                         edge::operator<'s (weight, b, a) order (SegmentTree.h:103-111); the sorted
 //                         edges come back to the host page-locked
-//   tree                  host: the reference builds it sequentially and so does this file: Kruskal with
+//   tree                  host: segment_graph's two passes, sequential as the reference's: Kruskal with
 //                         Felzenszwalb's size threshold, then the rest of the spanning tree with the
-//                         cross-segment penalty (segment-graph.h:48-101; disjoint-set.h:30-82); neighbour
-//                         lists in the sorted edge order, BFS from pixel 0 (SegmentTree.cpp:71-130)
+//                         cross-segment penalty (segment-graph.h:48-101; disjoint-set.h:30-82), as per-edge
+//                         marks.  GPU (round 4): the neighbour lists in the sorted edge order and the BFS
+//                         from pixel 0 (SegmentTree.cpp:71-130), by an Euler tour ranked with pointer
+//                         jumping and a depth sort (st_adj_kernel .. st_task_kernel, gpu_bfs)
 //   cost volume           GPU: truncated colour + gradient cost (StereoHelper.cpp:37-129), written
 //                         channel-major in BFS order, C[d][i], so a tree level is a contiguous run
 //   filter                GPU: one wave per disparity walks the BFS levels (st_filter_wave_kernel; one
@@ -1390,9 +1392,7 @@ struct TreeJob {
 
 // Neighbour-list storage of the host BFS path (the tree's own vector; its arrays take the page-locked
 // slot); the device path builds the lists on the GPU (null)
-AdjRec* list_storage(StWorkspace& ws, HostTree& t, int k, bool hbfs, int64_t P) {
-    (void)ws;
-    (void)k;
+AdjRec* list_storage(HostTree& t, bool hbfs, int64_t P) {
     if (!hbfs) return nullptr;
     t.adj.resize((size_t)P);
     return t.adj.data();
@@ -1589,7 +1589,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     HostTree* tp = nullptr;
     ST_CHK(host_tree_slot(ws, P, 0, tp, hbfs));
     HostTree& t = *tp;
-    AdjRec* adj = list_storage(ws, t, 0, hbfs, P);
+    AdjRec* adj = list_storage(t, hbfs, P);
     if (!host_tree_part(ws, 0, t, adj, hbfs, nE, P, W, tau, 1.0f)) {
         (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
@@ -1671,8 +1671,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(host_tree_slot(ws, P, 0, tlp, hbfs));
     ST_CHK(host_tree_slot(ws, P, 1, trp, hbfs));
     HostTree &tl = *tlp, &tr = *trp;
-    AdjRec* adjL = list_storage(ws, tl, 0, hbfs, P);
-    AdjRec* adjR = list_storage(ws, tr, 1, hbfs, P);
+    AdjRec* adjL = list_storage(tl, hbfs, P);
+    AdjRec* adjR = list_storage(tr, hbfs, P);
     float tab1[256];
     weight_table(kSigmaOne, tab1);
     std::vector<int4> tv[2];
@@ -1753,7 +1753,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     HostTree* tdp = nullptr;   // slot 0's tree object again
     ST_CHK(host_tree_slot(ws, P, 0, tdp, hbfs));
     HostTree& td = *tdp;
-    AdjRec* adjD = list_storage(ws, td, 0, hbfs, P);
+    AdjRec* adjD = list_storage(td, hbfs, P);
     if (!host_tree_part(ws, 0, td, adjD, hbfs, nE, P, W, tau, 255.0f)) {
         (void)hipStreamSynchronize(s);   // no copy into the page-locked buffers may outlive the call
         return hipErrorInvalidValue;
