@@ -114,16 +114,21 @@ __global__ __launch_bounds__(kST) void st_gradient_kernel(const uint8_t* __restr
 // column 0 (:107-110); double arithmetic as the reference's, rounded to float once.  RIGHT: the right
 // view's cost at pixel p = (y, x), GetRightMatchingCostFromLeft (StereoHelper.cpp:156-180): the left
 // cost at (y, min(x + d, W - 1)) and disparity min(d, W - 1 - x), whose right pixel is (y, x) itself.
+// One thread per BFS index i (pixel node[i]), so the D stores of a wave are coalesced (round 4: one thread
+// per pixel scattered them through rank; Art D = 60: 81 -> 51 us, rocprof); the image and gradient reads
+// gather from L2-resident rows instead.
 template <bool RIGHT>
 __global__ __launch_bounds__(kST) void st_cost_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                       int W, int H, int pitch, const float* __restrict__ gL,
-                                                      const float* __restrict__ gR, const int* __restrict__ rank, int D,
+                                                      const float* __restrict__ gR, const int* __restrict__ node, int D,
                                                       float* __restrict__ C) {
 #pragma clang fp contract(off)
-    const int x = blockIdx.x * kST + threadIdx.x, y = blockIdx.y;
-    if (x >= W) return;
-    const int64_t P = (int64_t)W * H, p = (int64_t)y * W + x;
-    const int i = rank[p];
+    const int64_t P = (int64_t)W * H;
+    const int i = blockIdx.x * kST + threadIdx.x;
+    if (i >= P) return;
+    const int p = node[i];
+    if ((unsigned)p >= (unsigned)P) return;
+    const int y = p / W, x = p - y * W;
     const double wc = 0.11, wg = 1.0 - wc;
     auto cost = [&](int xl, int xr) -> float {
         const uint8_t* l = L + (int64_t)y * pitch + 3 * xl;
@@ -1320,11 +1325,25 @@ hipError_t upload_tree(const HostTree& t, const float* table, int64_t P, DevTree
     return hipMemcpyAsync(d.table, table, 256 * sizeof(float), hipMemcpyHostToDevice, s);
 }
 
-// WTA of the filtered cost F (BFS order) of tree d into the map `out` (pixel order); node: P ints of scratch
-hipError_t launch_wta(const float* F, const DevTree& d, int* node, int P, int D, int scale, uint8_t* out, hipStream_t s) {
-    const dim3 g((unsigned)((P + kST - 1) / kST));
-    hipLaunchKernelGGL(st_node_kernel, g, dim3(kST), 0, s, d.rank, P, node);
-    hipLaunchKernelGGL(st_wta_kernel, g, dim3(kST), 0, s, F, node, P, D, scale, out);
+// node[i] of tree d (the inverse of its rank) into `node` (P ints), for the cost volume and the WTA
+hipError_t launch_node(const DevTree& d, int* node, int P, hipStream_t s) {
+    hipLaunchKernelGGL(st_node_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, d.rank, P, node);
+    return hipGetLastError();
+}
+
+// the cost volume in tree d's BFS order (node: launch_node's), RIGHT: the right view's
+template <bool RIGHT>
+hipError_t launch_cost(const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch, const float* grad, const int* node,
+                       int D, float* C, hipStream_t s) {
+    const int64_t P = (int64_t)W * H;
+    hipLaunchKernelGGL(st_cost_kernel<RIGHT>, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, dL, dR, W, H,
+                       pitch, grad, grad + P, node, D, C);
+    return hipGetLastError();
+}
+
+// WTA of the filtered cost F (BFS order) into the map `out` (pixel order); node: launch_node's
+hipError_t launch_wta(const float* F, const int* node, int P, int D, int scale, uint8_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(st_wta_kernel, dim3((unsigned)((P + kST - 1) / kST)), dim3(kST), 0, s, F, node, P, D, scale, out);
     return hipGetLastError();
 }
 
@@ -1603,9 +1622,8 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     const DevTree& dt = tj.d;
     float* C = ws.vol;
     float* F = ws.vol + (size_t)P * D;
-    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
-                       dt.rank, D, C);
-    ST_CHK(hipGetLastError());
+    ST_CHK(launch_node(dt, ws.node, (int)P, s));
+    ST_CHK(launch_cost<false>(dL, dR, W, H, pitch, ws.grad, ws.node, D, C, s));
     ST_CHK(read_trees(ws, hbfs, &tj, 1, P));
     const float tree_ms = ms_since(t0);
     FilterJobs jobs{};
@@ -1614,7 +1632,7 @@ hipError_t segment_tree_match(StWorkspace& ws, const uint8_t* dL, const uint8_t*
     wj.j[0] = wave_job(C, F, tj);
     ST_CHK(launch_filter(jobs, wj, 1, tj.maxw, D, (int)P, s));
     uint8_t* raw = ws.w8;   // the weights are consumed: reuse for the unfiltered map
-    ST_CHK(launch_wta(F, dt, ws.node, (int)P, D, scale, raw, s));
+    ST_CHK(launch_wta(F, ws.node, (int)P, D, scale, raw, s));
     ST_CHK(launch_median(raw, W, H, W, P, 1, 3, d_out, W, P, s));   // MeanFilter(disparity, disparity, 3)
     if (st) {
         st->levels = tj.d.nlev;
@@ -1720,11 +1738,10 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     float* F0 = ws.vol + (size_t)P * D;
     float* C1 = ws.vol + (size_t)P * D * 2;
     float* F1 = ws.vol + (size_t)P * D * 3;
-    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
-                       d0.rank, D, C0);
-    hipLaunchKernelGGL(st_cost_kernel<true>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
-                       d1.rank, D, C1);
-    ST_CHK(hipGetLastError());
+    ST_CHK(launch_node(d0, ws.node, (int)P, s));
+    ST_CHK(launch_node(d1, ws.node + P, (int)P, s));
+    ST_CHK(launch_cost<false>(dL, dR, W, H, pitch, ws.grad, ws.node, D, C0, s));
+    ST_CHK(launch_cost<true>(dL, dR, W, H, pitch, ws.grad, ws.node + P, D, C1, s));
     ST_CHK(read_trees(ws, hbfs, tj, 2, P));
     float tree_ms = ms_since(t0);
     FilterJobs jobs{};
@@ -1734,8 +1751,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     wj.j[0] = wave_job(C0, F0, tj[0]);
     wj.j[1] = wave_job(C1, F1, tj[1]);
     ST_CHK(launch_filter(jobs, wj, 2, std::max(tj[0].maxw, tj[1].maxw), D, (int)P, s));
-    ST_CHK(launch_wta(F0, d0, ws.node, (int)P, D, 1, raw0, s));
-    ST_CHK(launch_wta(F1, d1, ws.node + P, (int)P, D, 1, raw1, s));
+    ST_CHK(launch_wta(F0, ws.node, (int)P, D, 1, raw0, s));
+    ST_CHK(launch_wta(F1, ws.node + P, (int)P, D, 1, raw1, s));
     ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, mapL, W, P, s));   // MeanFilter(disparityLeft, ..., 3)
     ST_CHK(launch_median(raw1, W, H, W, P, 1, 3, mapR, W, P, s));
     // left-right check (StereoDisparity.cpp:129-147): mask = !occluded
@@ -1765,9 +1782,8 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     ST_CHK(enqueue_tree(ws, td, hbfs, P, W, nE, 255.0f, tab2, 0, s, tv2, t2));
     ST_CHK(mark_trees(ws, s));
     // second run on the same cost (the reference recomputes it, :150)
-    hipLaunchKernelGGL(st_cost_kernel<false>, rows, dim3(kST), 0, s, dL, dR, W, H, pitch, ws.grad, ws.grad + P,
-                       t2.d.rank, D, C0);
-    ST_CHK(hipGetLastError());
+    ST_CHK(launch_node(t2.d, ws.node, (int)P, s));
+    ST_CHK(launch_cost<false>(dL, dR, W, H, pitch, ws.grad, ws.node, D, C0, s));
     ST_CHK(read_trees(ws, hbfs, &t2, 1, P));
     tree_ms += ms_since(t0);
     FilterJobs job2{};
@@ -1775,7 +1791,7 @@ hipError_t segment_tree_refined_match(StWorkspace& ws, const uint8_t* dL, const 
     WaveJobs wj2{};
     wj2.j[0] = wave_job(C0, F0, t2);
     ST_CHK(launch_filter(job2, wj2, 1, t2.maxw, D, (int)P, s));
-    ST_CHK(launch_wta(F0, t2.d, ws.node, (int)P, D, scale, raw0, s));
+    ST_CHK(launch_wta(F0, ws.node, (int)P, D, scale, raw0, s));
     ST_CHK(launch_median(raw0, W, H, W, P, 1, 3, d_out, W, P, s));
     if (st) {
         st->levels = t2.d.nlev;
