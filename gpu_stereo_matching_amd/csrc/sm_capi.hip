@@ -403,6 +403,14 @@ bool zero_copy_enabled() {
     return on;
 }
 
+bool start_event_forced() {
+    static const bool on = [] {
+        const char* e = getenv("SM_START_EVENT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // SM_PAIR_COPY=0 (A/B only): a contiguous host pair still goes up as two copies
 bool pair_copy_enabled() {
     static const bool on = [] {
@@ -455,7 +463,12 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
     uint8_t* mapped = nullptr;
     if (zero_copy_enabled() && keep0 == 0 && keep1 == height && !right_out && !mask_out && !(flags & SM_LR_CHECK))
         mapped = host_block_device_ptr(disp_out, (size_t)(height - 1) * out_pitch + width);
-    SM_HIP(hipEventRecord(h->ev[0], s));
+    // stage split events (SM_PARAM_STAGE_TIMING): each costs a marker between the copy and compute
+    // queues, ~10 us per 1080p call for the two (profiles/microbench/r03_roundtrip_pair_block.txt); the
+    // start event likewise only when the split is recorded (round 4; SM_START_EVENT=1, read once, records
+    // it in every call as before, for A/B)
+    const bool ev = h->stage_timing == 1 || (h->stage_timing == 2 && (h->stage_requested || verbose_env()));
+    if (ev || start_event_forced()) SM_HIP(hipEventRecord(h->ev[0], s));
     // a pair with the right frame right after the left one (one sm_host_alloc block of 2 frames, or any
     // contiguous (2, H, W) array) goes up as one copy into d_left .. d_left + 2P: one DMA transfer
     // instead of two
@@ -468,9 +481,6 @@ int host_match_rows(sm_handle* h, const uint8_t* left, const uint8_t* right, int
         SM_HIP(copy2d(h->d_left, width, left, pitch, width, height, hipMemcpyHostToDevice, s));
         SM_HIP(copy2d(h->d_right, width, right, pitch, width, height, hipMemcpyHostToDevice, s));
     }
-    // stage split events (SM_PARAM_STAGE_TIMING): each costs a marker between the copy and compute
-    // queues, ~10 us per 1080p call for the two (profiles/microbench/r03_roundtrip_pair_block.txt)
-    const bool ev = h->stage_timing == 1 || (h->stage_timing == 2 && (h->stage_requested || verbose_env()));
     if (ev) SM_HIP(hipEventRecord(h->ev[1], s));
     rc = run_device(h, h->d_left, dR, width, height, width, 1, P, radius, num_disp, flags,
                     mapped ? mapped : h->d_disp, mapped ? out_pitch : width, P, right_out ? aux : nullptr,
