@@ -343,15 +343,30 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
 
 // run_device_body on stream s, ordered after the handle's previous pass when that ran on another
 // stream (the workspaces d_lr / d_rpart / d_vol are per handle).
+// A pass without median, LR or staged volumes touches no workspace: it neither waits for nor records the
+// scratch event (round 4: the marker cost the host call ~µs; SM_SCRATCH_EVENT=1, read once, keeps both for
+// every pass, for A/B)
+bool scratch_event_forced() {
+    static const bool on = [] {
+        const char* e = getenv("SM_SCRATCH_EVENT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
                uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
-    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    const bool uses_ws = (flags & (SM_STAGED | SM_MEDIAN | SM_LR_CHECK)) != 0 || right_out || mask_out ||
+                         scratch_event_forced();
+    if (uses_ws && h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
     const int rc = run_device_body(h, L, R, W, H, pitch, batch, fstride, radius, D, flags, disp, opitch, ostride,
                                    right_out, mask_out, apitch, astride, s);
-    SM_HIP(hipEventRecord(h->scratch_ev, s));
-    h->scratch_stream = s;
-    h->scratch_pending = true;
+    if (uses_ws) {
+        SM_HIP(hipEventRecord(h->scratch_ev, s));
+        h->scratch_stream = s;
+        h->scratch_pending = true;
+    }
     return rc;
 }
 

@@ -35,7 +35,8 @@ SETTINGS = {"dma": {"SM_ZERO_COPY": "0"}, "zc": {"SM_ZERO_COPY": "1"},
             "zc_pair_2copies": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_PAIR_COPY": "0"},
             "zc_pair_noev": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_AB_NOTIMING": "1"},
             # round 4: the start event recorded in every call (round 3) against only with the stage split
-            "zc_pair_startev": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_START_EVENT": "1"}}
+            "zc_pair_startev": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_START_EVENT": "1"},
+            "zc_pair_scratchev": {"SM_ZERO_COPY": "1", "SM_AB_PAIR": "1", "SM_SCRATCH_EVENT": "1"}}
 res = {k: [] for k in SETTINGS}
 for _ in range(3):
     for zc, env in SETTINGS.items():
@@ -49,7 +50,8 @@ for _ in range(3):
 for zc, name in (("dma", "DMA up + download"), ("zc", "DMA up + zero-copy map"),
                  ("zc_pair", "pair block, one copy + zc map"), ("zc_pair_2copies", "pair block, two copies + zc"),
                  ("zc_pair_noev", "pair block, one copy, no stage events"),
-                 ("zc_pair_startev", "pair block, start event every call")):
+                 ("zc_pair_startev", "pair block, start event every call"),
+                 ("zc_pair_scratchev", "pair block, scratch event every pass")):
     walls = [v[0] for v in res[zc]]
     print(f"{name:28s} wall ms/call median {statistics.median(walls):.4f} all {[round(w, 4) for w in walls]} "
           f"last stages upload/match/download {[round(x, 4) for x in res[zc][-1][1:]]}")
