@@ -22,7 +22,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 from . import _capi
-from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK, SM_MEDIAN, SM_STAGED  # noqa: F401
+from ._capi import SMError, SM_AGG_BOX, SM_AGG_GUIDED, SM_LR_CHECK, SM_MEDIAN, SM_STAGED, SM_DEVICE_CU_GRID  # noqa: F401
 from .synth import synth_pair  # noqa: F401
 from .gray import bgr_to_gray  # noqa: F401
 
@@ -46,10 +46,12 @@ def _as_u8_image(a, name: str) -> np.ndarray:
 
 
 def _flags(agg: str, lr_check: bool, median: bool = False) -> int:
-    """agg: 'box' (fused), 'box-staged' (through the AD / SAD volumes in HBM) or 'guided'."""
-    if agg not in ("box", "guided", "box-staged"):
-        raise ValueError("agg must be 'box', 'box-staged' or 'guided'")
-    f = {"box": SM_AGG_BOX, "guided": SM_AGG_GUIDED, "box-staged": SM_AGG_BOX | SM_STAGED}[agg]
+    """agg: 'box' (fused), 'box-staged' (through the AD / SAD volumes in HBM), 'guided', or 'device-cu'
+    (Device.cu's literal output with its fixed launch geometry: SM_DEVICE_CU_GRID, box only)."""
+    if agg not in ("box", "guided", "box-staged", "device-cu"):
+        raise ValueError("agg must be 'box', 'box-staged', 'guided' or 'device-cu'")
+    f = {"box": SM_AGG_BOX, "guided": SM_AGG_GUIDED, "box-staged": SM_AGG_BOX | SM_STAGED,
+         "device-cu": SM_DEVICE_CU_GRID}[agg]
     return f | (SM_LR_CHECK if lr_check else 0) | (SM_MEDIAN if median else 0)
 
 

@@ -23,6 +23,7 @@ SM_AGG_GUIDED = 1
 SM_LR_CHECK = 2
 SM_MEDIAN = 4
 SM_STAGED = 8
+SM_DEVICE_CU_GRID = 16
 
 SM_PARAM_GUIDED_EPS = 1
 SM_PARAM_STAGED_GROUP = 2

@@ -74,6 +74,11 @@ hipError_t launch_all_sad_generic(const uint8_t* L, const uint8_t* R, int W, int
 // (`frames` consecutive frames of D planes each; frame f's map at disp + f * out_stride)
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,
                              int out_pitch, int64_t out_stride, hipStream_t s);
+// SM_DEVICE_CU_GRID (bm_literal.hip): Device.cu's literal map, AD only for rows < 256 and cols < 320, all zero
+// for W > 1024; needs W >= 320, H >= 256 and literal_workspace_bytes(D) of device scratch in `ws`
+size_t literal_workspace_bytes(int D);
+hipError_t launch_device_cu_literal(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int radius, int D,
+                                    uint32_t* ws, uint8_t* out, int opitch, hipStream_t s);
 // (2r+1)^2 median with replicate borders, radius 1..3 (bm_post.hip)
 hipError_t launch_median(const uint8_t* src, int W, int H, int pitch, int64_t stride, int batch, int radius,
                          uint8_t* dst, int dpitch, int64_t dstride, hipStream_t s);

@@ -243,6 +243,21 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     const int64_t PB = P * batch;
     const bool fused_right = lr && !guided && radius <= sm::kMaxBoxRadius;
     const bool guided_right = lr && guided;   // right view fused into the guided pass (bm_guided.hip)
+    if ((flags & SM_DEVICE_CU_GRID) != 0) {   // Device.cu's launch geometry, frame by frame (bm_literal.hip)
+        if (flags != SM_DEVICE_CU_GRID || lr)
+            return fail(SM_ERR_INVALID_ARG, "SM_DEVICE_CU_GRID is box aggregation only (flags 0x%x)", flags);
+        if (W < 320 || H < 256)
+            return fail(SM_ERR_INVALID_ARG,
+                        "SM_DEVICE_CU_GRID: %dx%d is below the 320x256 the reference's fixed grid assumes "
+                        "(Device.cu:231-233 reads and writes outside the frame)", W, H);
+        int rc = ensure_vol(h, sm::literal_workspace_bytes(D));
+        if (rc) return rc;
+        for (int f = 0; f < batch; ++f)
+            SM_HIP(sm::launch_device_cu_literal(L + f * fstride, R + f * fstride, W, H, pitch, radius, D,
+                                                reinterpret_cast<uint32_t*>(h->d_vol), disp + f * ostride, opitch,
+                                                s));
+        return SM_OK;
+    }
     if ((flags & SM_STAGED) != 0) {
         if (guided || lr || radius > sm::kMaxFastRadius)
             return fail(SM_ERR_INVALID_ARG, "SM_STAGED supports box aggregation without LR, radius <= %d",
@@ -357,7 +372,7 @@ bool scratch_event_forced() {
 int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
                uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
-    const bool uses_ws = (flags & (SM_STAGED | SM_MEDIAN | SM_LR_CHECK)) != 0 || right_out || mask_out ||
+    const bool uses_ws = (flags & (SM_STAGED | SM_MEDIAN | SM_LR_CHECK | SM_DEVICE_CU_GRID)) != 0 || right_out || mask_out ||
                          scratch_event_forced();
     if (uses_ws && h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
     const int rc = run_device_body(h, L, R, W, H, pitch, batch, fstride, radius, D, flags, disp, opitch, ostride,
@@ -878,6 +893,8 @@ int group_bands(sm_group* g, const uint8_t* left, const uint8_t* right, int widt
                 int out_pitch) {
     if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
     if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (flags & SM_DEVICE_CU_GRID)   // the literal grid is anchored at the frame's corner: not row-local
+        return fail(SM_ERR_INVALID_ARG, "SM_DEVICE_CU_GRID needs whole frames (sm_group_block_match_batch_u8)");
     if (width <= 0 || height <= 0 || pitch < width || out_pitch < width)
         return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d pitch %d out_pitch %d", width, height, pitch,
                     out_pitch);
@@ -1670,6 +1687,8 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
                                           uint8_t* disp_out, int out_pitch) {
     if (!g) return fail(SM_ERR_INVALID_ARG, "null group");
     if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
+    if (flags & SM_DEVICE_CU_GRID)   // the literal grid is anchored at the frame's corner: not row-local
+        return fail(SM_ERR_INVALID_ARG, "SM_DEVICE_CU_GRID needs whole frames (sm_group_block_match_batch_u8)");
     if (width <= 0 || height <= 0 || pitch < width || out_pitch < width)
         return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d pitch %d out_pitch %d", width, height, pitch,
                     out_pitch);

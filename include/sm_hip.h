@@ -50,7 +50,7 @@ enum {
                                MeanFilter(disp, disp, 3) = ctmf (Toolkit.cpp:33-48); with
                                SM_LR_CHECK both maps are filtered before the check, in the
                                order of StereoDisparity.cpp:119-126 */
-    SM_STAGED = 8u          /* box path through explicit HBM volumes (AD u8 -> SAD u16 -> WTA),
+    SM_STAGED = 8u,         /* box path through explicit HBM volumes (AD u8 -> SAD u16 -> WTA),
                                the reference's two-kernel data flow (Device.cu:19-64); same
                                output as the fused kernel, bandwidth-bound; not with
                                SM_AGG_GUIDED or SM_LR_CHECK, radius <= 7.  Frames run in launch
@@ -60,6 +60,14 @@ enum {
                                ~0.8 GB with groups of 1.  Lowering SM_PARAM_STAGED_GROUP frees the
                                workspace (after the handle's pending work), so the next staged call
                                allocates the smaller size */
+    SM_DEVICE_CU_GRID = 16u /* opt-in emulation of Device.cu's fixed launch geometry (Device.cu:231-233,
+                               253): the AD cost only for rows < 256 and cols < 320, 0 elsewhere (the
+                               memset, :193-194), and the all-zero map for width > 1024 (the failed
+                               <<<rows, cols>>> launch, :191-192).  Equals the default map at exactly
+                               320x256; width < 320 or height < 256 (where the reference reads and writes
+                               out of bounds) is SM_ERR_INVALID_ARG.  Box aggregation only (no other flag);
+                               whole frames only (not the row-band or d-slice group calls).  Uses
+                               ~330 KB * num_disp of the handle's volume workspace */
 };
 
 /* ---- scalar parameters (sm_set_param_f) ---- */

@@ -146,8 +146,6 @@ struct Engine {
             h = nullptr;
             return false;
         }
-        // the stage lines read the upload / match / download split of every call
-        if (!quiet()) sm_set_param_f(h, SM_PARAM_STAGE_TIMING, 1.f);
         // the d-slice mode runs through a group even on one device (a one-rank communicator)
         const char* mode = std::getenv("SM_GROUP_MODE");
         std::vector<int> gdevs = devs;
@@ -189,8 +187,16 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     if (!e.ensure(cols, rows, searchRange)) return SM_ERR_DEVICE;
     const char* mode = std::getenv("SM_GROUP_MODE");
     const bool dslice = e.g && mode && std::string(mode) == "dslice" && (flags & ~(unsigned)SM_AGG_GUIDED) == 0u;
+    // the stage lines read the upload / match / download split of this call only: the handle stays at the
+    // auto default (no event markers) for testBM / getDisp / PreCal / getAllSAD
+    const bool timed = stage_lines && !detail::quiet() && !e.g;
+    if (timed) sm_set_param_f(e.h, SM_PARAM_STAGE_TIMING, 1.f);
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = dslice ? sm_group_dslice_block_match_u8(e.g, h_left.data, h_right.data, cols, rows,
+    // Device.cu's literal launch geometry (SM_DEVICE_CU_GRID) is a whole-frame pass: one device
+    int rc = (flags & SM_DEVICE_CU_GRID) ? sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows,
+                                                             (int)detail::row_step(h_left), SADWindowSize, searchRange,
+                                                             flags, h_disparity.data, (int)detail::row_step(h_disparity))
+             : dslice ? sm_group_dslice_block_match_u8(e.g, h_left.data, h_right.data, cols, rows,
                                                      (int)detail::row_step(h_left), SADWindowSize, searchRange, flags,
                                                      h_disparity.data, (int)detail::row_step(h_disparity))
              : e.g ? sm_group_block_match_u8(e.g, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
@@ -199,6 +205,7 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
                  : sm_block_match_u8(e.h, h_left.data, h_right.data, cols, rows, (int)detail::row_step(h_left),
                                      SADWindowSize, searchRange, flags, h_disparity.data,
                                      (int)detail::row_step(h_disparity));
+    if (timed) sm_set_param_f(e.h, SM_PARAM_STAGE_TIMING, 2.f);
     if (rc != SM_OK) {
         std::cerr << "blockMatching_gpu: " << sm_last_error_string() << std::endl;
         for (int r = 0; r < rows; ++r) std::memset(h_disparity.data + (size_t)r * detail::row_step(h_disparity), 0, cols);
@@ -206,7 +213,7 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     }
     if (stage_lines && !detail::quiet()) {
         float up = 0, mt = 0, dn = 0;
-        if (e.g)   // row bands / d-slices on several devices: one wall time, no single copy stage
+        if (e.g && !(flags & SM_DEVICE_CU_GRID))   // row bands / d-slices on several devices: one wall time
             mt = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
         else
             sm_last_stage_ms(e.h, &up, &mt, &dn);
@@ -257,9 +264,14 @@ using SmHostMat = cv::Mat;
 #else
 using SmHostMat = sm::Mat;
 #endif
+// SM_DEVICE_CU_GRID=1 in the environment reproduces Device.cu's literal output, launch geometry included
+// (AD only for rows < 256, cols < 320; all zero for cols > 1024: Device.cu:231-233, 253); the default is the
+// intended getDisp semantics at every size.
 inline void blockMatching_gpu(SmHostMat& h_left, SmHostMat& h_right, SmHostMat& h_disparity, int SADWindowSize,
                               int searchRange) {
-    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange, SM_AGG_BOX, true);
+    const char* lit = std::getenv("SM_DEVICE_CU_GRID");
+    const unsigned flags = (lit && lit[0] == '1') ? (unsigned)SM_DEVICE_CU_GRID : (unsigned)SM_AGG_BOX;
+    sm::block_matching(h_left, h_right, h_disparity, SADWindowSize, searchRange, flags, true);
 }
 inline void remap_gpu(SmHostMat& left, SmHostMat& right, SmHostMat& mapX1, SmHostMat& mapY1, SmHostMat& mapX2,
                       SmHostMat& mapY2, int rows, int cols, int /*total*/, uchar* result) {

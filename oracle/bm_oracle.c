@@ -265,6 +265,71 @@ ORA_API int ora_get_all_sad(const uint8_t *L, const uint8_t *R, int W, int H, in
 }
 
 /* ------------------------------------------------------------------------- */
+/* a1+a2 as Device.cu actually launches them (blockMatching_gpu, :173-301),  */
+/* launch geometry included:                                                  */
+/*  - d_disparity and d_difference are memset to 0 (:191-194);                */
+/*  - kernalPreCal_V2 runs on grid (8, 10, D) x block (32, 32) (:231-233):    */
+/*    rowIndex = blockIdx.x*32 + threadIdx.x < 256, colIndex = blockIdx.y*32  */
+/*    + threadIdx.y < 320 (:21-22), so only rows < 256, cols < 320 get an AD  */
+/*    value (:27-31); the rest of every plane keeps the memset 0;             */
+/*  - kernalFindCorr runs <<<rows, cols>>> (:253): one thread per pixel, the  */
+/*    getDisp rule without the early exit (:36-63).  A block of more than     */
+/*    1024 threads does not launch, so for cols > 1024 the map stays the      */
+/*    memset 0 (the reference checks no error).                               */
+/* rows < 256 or cols < 320 make the fixed grid read and write outside the    */
+/* frame (frameBias up to 255*cols + 319 >= rows*cols): undefined in the      */
+/* reference, rejected here (returns -2).  At exactly 320x256 the grid covers */
+/* every (row, col, d) and this equals ora_get_disp.                          */
+/* ------------------------------------------------------------------------- */
+ORA_API int ora_device_cu_literal(const uint8_t *L, const uint8_t *R, int W, int H, int radius, int D,
+                                  uint8_t *out)
+{
+    const int64_t total = (int64_t)W * H;
+    if (W < 320 || H < 256) return -2;
+    memset(out, 0, (size_t)total);                          /* :191-192 */
+    if (W > 1024) return 0;                                 /* :253 launch failure */
+    uint8_t *dif = (uint8_t *)calloc((size_t)(total * D), 1); /* :193-194 */
+    if (!dif) return -1;
+    for (int z = 0; z < D; ++z)                             /* grid.z = frameIndex */
+        for (int bx = 0; bx < 8; ++bx)
+            for (int by = 0; by < 10; ++by)
+                for (int tx = 0; tx < 32; ++tx)
+                    for (int ty = 0; ty < 32; ++ty) {
+                        const int colIndex = by * 32 + ty;  /* :21 */
+                        const int rowIndex = bx * 32 + tx;  /* :22 */
+                        const int64_t frameBias = (int64_t)rowIndex * W + colIndex; /* :23 */
+                        const int64_t index = (int64_t)z * total + frameBias;       /* :25 */
+                        if (colIndex - z >= 0) {            /* :27-28 */
+                            int v = (int)L[frameBias] - (int)R[frameBias - z];
+                            dif[index] = (uint8_t)(v < 0 ? -v : v);             /* :30 */
+                        }
+                    }
+    const int windowArea = (2 * radius + 1) * (2 * radius + 1);
+    for (int64_t t = 0; t < total; ++t) {                   /* threadIndex, :36 */
+        int best = 50 * windowArea;                         /* :37 */
+        int dm = -256;                                      /* :38 */
+        const int col = (int)(t % W), row = (int)(t / W);   /* :39-40 */
+        int64_t th = 0;
+        for (int s = 0; s < D; ++s, th += total) {          /* :43 */
+            if (col + s > W) break;                         /* :44 */
+            int sad = 0;
+            for (int i = -radius; i <= radius; ++i)
+                for (int j = -radius; j <= radius; ++j) {
+                    const int c = col + j;
+                    if (c >= W || c < 0) continue;          /* :51 */
+                    const int rr = row + i;
+                    if (rr >= H || rr < 0) continue;        /* :53 */
+                    sad += dif[th + t + (int64_t)W * i + j]; /* :54 */
+                }
+            if (sad < best) { dm = s; best = sad; }         /* :57-60 */
+        }
+        out[t] = (uint8_t)dm;                               /* :63 */
+    }
+    free(dif);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* a3: independent restatement of the same map as                            */
 /*   zero-padded (2r+1)^2 box sum of each AD plane                           */
 /*   + validity d <= W - x (the break at BlockMatching.cpp:166/Device.cu:44) */

@@ -43,6 +43,8 @@ def lib():
         L.ora_precal.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p]
         L.ora_get_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _u8p]
         L.ora_get_all_sad.argtypes = L.ora_get_disp.argtypes
+        L.ora_device_cu_literal.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p]
+        L.ora_device_cu_literal.restype = ctypes.c_int
         L.ora_get_disp.restype = ctypes.c_int
         L.ora_box_disp.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _i32p, _u32p]
         L.ora_box_disp.restype = ctypes.c_int
@@ -122,6 +124,53 @@ def get_disp(left, right, sad_window_size: int, search_range: int) -> np.ndarray
     if rc != 0:
         raise MemoryError("ora_get_disp")
     return out
+
+
+def device_cu_literal(left, right, sad_window_size: int, search_range: int) -> np.ndarray:
+    """Device.cu's map as its fixed launch geometry produces it (blockMatching_gpu, Device.cu:173-301):
+    the AD volume only for rows < 256 and cols < 320 (grid (8,10,D) x block (32,32), :231-233; 0 elsewhere
+    from the memset, :193-194), the all-zero map for cols > 1024 (the <<<rows, cols>>> launch fails, :253).
+    Raises ValueError for rows < 256 or cols < 320, where the reference reads and writes out of bounds."""
+    left, right = _img(left), _img(right)
+    H, W = left.shape
+    out = np.empty((H, W), np.uint8)
+    rc = lib().ora_device_cu_literal(_p(left, _u8p), _p(right, _u8p), W, H, sad_window_size, search_range,
+                                     _p(out, _u8p))
+    if rc == -2:
+        raise ValueError(f"{W}x{H}: the Device.cu launch grid is out of bounds below 320x256")
+    if rc != 0:
+        raise MemoryError("ora_device_cu_literal")
+    return out
+
+
+def device_cu_literal_integral(left, right, radius: int, D: int) -> np.ndarray:
+    """Second, independent formulation of device_cu_literal (numpy, for cross-checking the C loop nest):
+    the AD planes masked to the grid's 256 x 320 coverage, 2-D integral images, clipped window sums by
+    four lookups, then the strict-< WTA from 50 * win^2 with the col + d > W break."""
+    L = _img(left).astype(np.int64)
+    Rr = _img(right).astype(np.int64)
+    H, W = L.shape
+    if W < 320 or H < 256:
+        raise ValueError("below 320x256")
+    out = np.zeros((H, W), np.uint8)
+    if W > 1024:
+        return out
+    win = 2 * radius + 1
+    best = np.full((H, W), 50 * win * win, np.int64)
+    dm = np.full((H, W), -256, np.int64)
+    ys, xs = np.mgrid[0:H, 0:W]
+    y0, y1 = np.clip(ys - radius, 0, H), np.clip(ys + radius + 1, 0, H)
+    x0, x1 = np.clip(xs - radius, 0, W), np.clip(xs + radius + 1, 0, W)
+    for d in range(D):
+        ad = np.zeros((H, W), np.int64)
+        ad[:256, d:320] = np.abs(L[:256, d:320] - Rr[:256, 0:320 - d]) if d < 320 else 0
+        I = np.zeros((H + 1, W + 1), np.int64)
+        I[1:, 1:] = ad.cumsum(0).cumsum(1)
+        sad = I[y1, x1] - I[y0, x1] - I[y1, x0] + I[y0, x0]
+        upd = (sad < best) & (xs + d <= W)
+        best = np.where(upd, sad, best)
+        dm = np.where(upd, d, dm)
+    return (dm & 0xFF).astype(np.uint8)
 
 
 def get_all_sad(left, right, sad_window_size: int, search_range: int) -> np.ndarray:

@@ -202,3 +202,17 @@ def test_blockmatching_h_api_cpp(tmp_path, gray, bm_expected, oracle, pair, sad)
     assert [ln for ln in sec["compareDisp planted"] if ln.startswith(("[", "CPU"))] == \
         ["[1:2]", f"CPU = {d}, GPU = {d ^ 1}"]
     assert [ln for ln in sec["compareSAD planted"] if not ln.startswith(("prep", "precalculate"))] == ["5", "-1"]
+
+
+@pytest.mark.gpu
+def test_single_frame_cpp_device_cu_grid(tmp_path, gray):
+    """SM_DEVICE_CU_GRID=1: an unchanged blockMatching_gpu caller gets Device.cu's literal map (its fixed
+    launch grid covers rows < 256, cols < 320 only, Device.cu:231-233) on a 463x370 bundled pair."""
+    exp = np.load(os.path.join(ROOT, "tests", "golden", "device_cu_expected.npz"))
+    _write_pgm(tmp_path / "l.pgm", gray["Books/view1"])
+    _write_pgm(tmp_path / "r.pgm", gray["Books/view5"])
+    env = dict(os.environ, SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
+               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD="4", SM_RANGE="64", SM_QUIET="1", SM_DEVICE_CU_GRID="1")
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_read_pgm(tmp_path / "d.pgm"), exp["Books/r4/D64"])

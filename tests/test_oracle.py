@@ -279,3 +279,32 @@ def test_get_all_sad_golden_pair(oracle, gray):
     valid = np.broadcast_to(x + d <= L.shape[1], vol.shape)
     assert np.array_equal(vol[valid], (full[valid] & 0xFF).astype(np.uint8))
     assert (vol[~valid] == 255).all()
+
+
+def test_device_cu_literal_two_restatements_and_survey_counts(oracle, gray):
+    """Device.cu's literal map (launch geometry included, Device.cu:191-194, 231-233, 253): the loop nest
+    over the (8, 10, D) x (32, 32) grid (ora_device_cu_literal) equals the numpy integral-image
+    formulation, equals getDisp at 320x256, and differs from getDisp on exactly the pixel counts
+    SURVEY §8a a1 measured independently at r = 4, D = 64: Art 85,893, Books 83,551 of 171,310."""
+    L, R = gray["Art_/view1"], gray["Art_/view5"]
+    lit = oracle.device_cu_literal(L, R, 5, 64)
+    assert np.array_equal(lit, oracle.get_disp(L, R, 5, 64))
+    for p, n in (("Art", 85893), ("Books", 83551)):
+        L, R = gray[f"{p}/view1"], gray[f"{p}/view5"]
+        lit = oracle.device_cu_literal(L, R, 4, 64)
+        assert np.array_equal(lit, oracle.device_cu_literal_integral(L, R, 4, 64))
+        assert int((lit != oracle.box_disp(L, R, 4, 64)).sum()) == n
+
+
+def test_device_cu_literal_golden_and_edges(oracle, gray):
+    import os
+    from conftest import GOLDEN
+    exp = np.load(os.path.join(GOLDEN, "device_cu_expected.npz"))
+    L, R = gray["Dolls/view1"], gray["Dolls/view5"]
+    assert np.array_equal(oracle.device_cu_literal_integral(L, R, 0, 32), exp["Dolls/r0/D32"])
+    A, B = oracle.synth_pair(5, 1030, 256, 32)
+    assert not oracle.device_cu_literal(A, B, 2, 32).any()          # cols > 1024: the launch fails
+    with pytest.raises(ValueError):
+        oracle.device_cu_literal(A[:, :319], B[:, :319], 2, 32)     # below the grid's 320 x 256
+    with pytest.raises(ValueError):
+        oracle.device_cu_literal(A[:255], B[:255], 2, 32)
