@@ -57,21 +57,12 @@ constexpr int kNB = kTileH / 16;   // 16-row CS hand-off blocks per tile
 constexpr int kPairs = 4;
 constexpr int kChunk = 2 * kPairs;
 constexpr int kCols = 64;
-// right-key partial rows: 16-B aligned groups of 4 u, reduced with 16-B loads (SM_RR_VEC=0: one
-// 4-B load per u and tile, the round-3 layout)
-#ifndef SM_RR_VEC
-#define SM_RR_VEC 1
-#endif
-constexpr bool kRrVec = SM_RR_VEC != 0;
-// right-key rows skewed against bank conflicts of the scatter (Geo::RB_SKEW; SM_RB_SKEW=0: unskewed rows)
-#ifndef SM_RB_SKEW
-#define SM_RB_SKEW 1
-#endif
-constexpr bool kRbSkew = SM_RB_SKEW != 0;
+// right-key partial rows: 16-B aligned groups of 4 u, reduced with 16-B loads (round 3; one 4-B load per u
+// and tile before), rows skewed against the scatter's bank conflicts (round 4, Geo::RB_SKEW)
 
 // pad slots in front of tile tx's partial row: lead + (u - tx*TW + dmax + 1) == 0 (mod 4) for u == 0 (mod 4)
 __host__ __device__ constexpr int rr_lead(int tx, int TW, int dmax) {
-    return kRrVec ? 1 + ((((tx * TW - dmax - 1) - 1) % 4 + 4) % 4) : 0;
+    return 1 + ((((tx * TW - dmax - 1) - 1) % 4 + 4) % 4);
 }
 
 template <int R, int DMAX, int NW = 4>
@@ -104,9 +95,9 @@ struct Geo {
     // fused right view (RIGHT kernels): per-tile right-key rows indexed by u - (x0 - DMAX - 1);
     // row stride == 1 (mod 64) keeps the 64 lanes of a scatter on distinct banks (2-way for NQ 14)
     static constexpr int PW = TW + DMAX + 1;                    // right-key entries per partial row
-    // partial row in HBM (SM_RR_VEC): the PW entries behind lead(tx) in 1..4 pad slots, so that the
+    // partial row in HBM: the PW entries behind lead(tx) in 1..4 pad slots, so that the
     // entry of every u = 0 (mod 4) is 16-B aligned in every tile's row; pads are neutral (0xFFFFFFFF)
-    static constexpr int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;
+    static constexpr int PWP = (PW + 7 + 3) & ~3;
     static constexpr int RBW = ((PW + 63) / 64) * 64 + 1;       // >= PW + 1
     // row j starts at rb_row(j) = j * RBW + skew(j): a scatter's 32-lane group is rows hj = 0..15 of two
     // quarter-rows 14 columns apart (NQ = 14), so the row starts must cover the banks = 0, 1 (mod 4)
@@ -115,7 +106,7 @@ struct Geo {
     // overlapped by 4 entries when the skew restarted at 0).  With RBW = 1 (mod 32) alone, rows 14, 15 of
     // one quarter met rows 0, 1 of the next: every ds_min_u32 2-way conflicted (rocprof: 17 % of the
     // kernel's LDS cycles were bank conflicts; 1.5 % with the skew)
-    static constexpr int RB_SKEW = kRbSkew ? 2 : 0;
+    static constexpr int RB_SKEW = 2;
     static constexpr int RB_BYTES = ((kTileH * RBW + 15 * RB_SKEW) * 4 + 15) & ~15;
     static constexpr int LDS_BYTES_R = LDS_BYTES + RB_BYTES;
     static_assert(NQ % 4 == 2 || NQ % 4 == 0, "NQ even");
@@ -476,50 +467,7 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
 // partial rows cover u (x0 - DMAX - 1 <= u < x0 + TW, x0 <= u + d_hi - 1); dR = key & 0xFF with no
 // threshold (StereoHelper.cpp:131-154).  Then StereoDisparity.cpp:136-147 on the row:
 //   d = dL(x); occ = x-d < 0 || d == 0 || |d - dR(x-d)| > 1;  out = occ ? 0 : d.
-template <int MAXT>
-__global__ __launch_bounds__(256) void right_reduce_lr_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
-                                                              int tiles_y, int TW, int PW, int dmax, int d_hi, int W,
-                                                              int H, int check, uint8_t* disp, int opitch, int64_t ostride,
-                                                              uint8_t* __restrict__ right_out,
-                                                              uint8_t* __restrict__ mask_out, int apitch,
-                                                              int64_t astride) {
-    extern __shared__ uint8_t dr_row[];
-    const int y = blockIdx.x, f = blockIdx.y;
-    const int ty = y / kTileH, j = y - ty * kTileH;
-    const uint32_t* base = rpart + (((int64_t)f * tiles_y + ty) * tiles_x * kTileH + j) * PW;
-    const int64_t tstride = (int64_t)kTileH * PW;
-    uint8_t* rrow = right_out ? right_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
-    for (int u = threadIdx.x; u < W; u += blockDim.x) {
-        const int tlo = u / TW;
-        const int thi = min(tiles_x - 1, (u + d_hi - 1) / TW);
-        // at most MAXT tiles cover u: fixed trip count, so all the loads issue before the first use
-        uint32_t key = 0xFFFFFFFFu;
-#pragma unroll
-        for (int k = 0; k < MAXT; ++k) {
-            const int tx = tlo + k;
-            if (tx <= thi) key = min(key, base[tx * tstride + (u - tx * TW + dmax + 1)]);
-        }
-        const uint8_t dr = (uint8_t)(key & 0xFFu);
-        dr_row[u] = dr;
-        if (rrow) rrow[u] = dr;
-    }
-    if (!check) return;
-    __syncthreads();
-    uint8_t* drow = disp + (int64_t)f * ostride + (int64_t)y * opitch;
-    uint8_t* mrow = mask_out ? mask_out + (int64_t)f * astride + (int64_t)y * apitch : nullptr;
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        const int d = drow[x];
-        int occ = 1;
-        if (x - d >= 0) {
-            const int diff = d - (int)dr_row[x - d];
-            occ = (d == 0) || diff > 1 || diff < -1;
-        }
-        drow[x] = occ ? (uint8_t)0 : (uint8_t)d;
-        if (mrow) mrow[x] = (uint8_t)!occ;
-    }
-}
-
-// The same with the padded partial rows (SM_RR_VEC): a thread takes u = 4m..4m+3 and reads each covering
+// The partial rows are padded (Geo::PWP): a thread takes u = 4m..4m+3 and reads each covering
 // tile's four entries with one 16-B load.  The tile range is that of the group (a tile covering only some
 // of the four u holds 0xFFFFFFFF or a valid candidate of the others: every entry a tile writes is
 // C_L(u + d, d) of one of its pixels, so a min over a superset of the covering tiles is the same key).
@@ -665,20 +613,12 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
                            (size_t)G::LDS_BYTES_R, s, a, tiles_x, tiles_y);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if constexpr (kRrVec) {
-            // tiles covering one of u .. u + 3: ceil((d_hi + 2) / TW) + 1 at most
-            constexpr int kMaxT4 = (DMAX + 2 + G::TW - 1) / G::TW + 1;
-            hipLaunchKernelGGL((right_reduce_lr_vec_kernel<kMaxT4>), dim3(a.H, batch), dim3(256),
-                               (size_t)((a.W + 3) & ~3), s, a.rpart, tiles_x, tiles_y, G::TW, G::PWP, DMAX, a.d_hi,
-                               a.W, a.H, ro->check, a.disp, a.out_pitch, a.out_frame_stride, ro->right, ro->mask,
-                               ro->pitch, ro->stride);
-        } else {
-            // tiles covering one u: (TW + d_hi - 1) / TW + 1 at most
-            constexpr int kMaxT = (G::TW + DMAX - 1) / G::TW + 1;
-            hipLaunchKernelGGL((right_reduce_lr_kernel<kMaxT>), dim3(a.H, batch), dim3(256), (size_t)a.W, s, a.rpart,
-                               tiles_x, tiles_y, G::TW, G::PW, DMAX, a.d_hi, a.W, a.H, ro->check, a.disp, a.out_pitch,
-                               a.out_frame_stride, ro->right, ro->mask, ro->pitch, ro->stride);
-        }
+        // tiles covering one of u .. u + 3: ceil((d_hi + 2) / TW) + 1 at most
+        constexpr int kMaxT4 = (DMAX + 2 + G::TW - 1) / G::TW + 1;
+        hipLaunchKernelGGL((right_reduce_lr_vec_kernel<kMaxT4>), dim3(a.H, batch), dim3(256),
+                           (size_t)((a.W + 3) & ~3), s, a.rpart, tiles_x, tiles_y, G::TW, G::PWP, DMAX, a.d_hi,
+                           a.W, a.H, ro->check, a.disp, a.out_pitch, a.out_frame_stride, ro->right, ro->mask,
+                           ro->pitch, ro->stride);
     } else {
         // no more tiles than CUs (a small frame, batch 1): 16 waves per tile, >= 2 d-pairs each, so every
         // CU runs 16 waves instead of <= 4 (R <= 7: the wide-radius kernels need > 128 VGPRs).  Beyond
@@ -724,7 +664,7 @@ size_t partial_bytes_r(int W, int H, int D, int batch) {
     const int dmax = dspan <= 64 ? 64 : (dspan <= 128 ? 128 : (dspan <= 192 ? 192 : 256));
     const int TW = kCols - 2 * R;
     const int PW = TW + dmax + 1;
-    const int PWP = kRrVec ? ((PW + 7 + 3) & ~3) : PW;   // Geo::PWP
+    const int PWP = (PW + 7 + 3) & ~3;   // Geo::PWP
     const size_t tiles = (size_t)((W + TW - 1) / TW) * ((H + kTileH - 1) / kTileH);
     return tiles * (size_t)batch * kTileH * PWP * 4;
 }

@@ -92,29 +92,15 @@ constexpr uint32_t kPLow = kPOne - 1;
 #endif
 constexpr bool kGuidedRoles = SM_G_ROLES != 0;
 
-// Tall tiles (round 4): 48 output rows on 6 waves instead of 32 on 4.  The P halo
-// per output drops from 64 x 52 / (44 x 32) = 2.36 to 64 x 68 / (44 x 48) = 2.06 and the A halo from
-// 1.61 to 1.48 (r = 5); the LDS plan grows to ~71 KB, so two workgroups share a CU: 12 waves, as three
-// 4-wave workgroups had.  Measured (round 4, same box, 1080p D=128 r=5, 32 frames per call, us per
-// frame): guided 453.3 (32-row tiles) -> 851.0 (tall), guided + LR 524.7 -> 953.2 with the right view
-// tall too (SM_G_TALL_RIGHT), no spills in either (168 / 160 VGPRs).  A dead end: off by default, kept
-// as an A/B switch (profiles/microbench/r04_guided_tall_ab.txt).
-// SM_G_TALL=2: 96-row tiles on one 12-wave workgroup per CU (3, 3, 3, 3 waves on the SIMDs, the
-// occupancy of three 4-wave workgroups): P halo 64 x 116 / (44 x 96) = 1.76, A halo 1.36, 133 KB of LDS.
-#ifndef SM_G_TALL
-#define SM_G_TALL 0
-#endif
-template <int R>
-constexpr bool kGuidedTall = SM_G_TALL != 0 && R >= 1 && R <= 5;
-constexpr int kTallKind = SM_G_TALL;
-
-// TALL: 0 = 32-row tiles on 4 waves, 1 = 48 rows on 6 waves, 2 = 96 rows on 12 waves
-template <int R, bool ROLES = kGuidedRoles, int TALL = 0>
+// Taller tiles (round 4: 48 rows on 6 waves, 96 rows on one 12-wave workgroup per CU) cut the halo but
+// lost occupancy and ran 1.9x / 1.3x slower; the variants were removed in round 5
+// (git history: SM_G_TALL / SM_G_TALL_RIGHT before commit "guided: drop the measured tall-tile variants").
+template <int R, bool ROLES = kGuidedRoles>
 struct GeoF {
-    static constexpr int NT = TALL == 2 ? 768 : TALL ? 384 : kT;   // threads per workgroup
+    static constexpr int NT = kT;                            // threads per workgroup
     static constexpr int NWV = NT / 64;                      // waves per workgroup
     static constexpr int TW = 64 - 4 * R;
-    static constexpr int TH = TALL == 2 ? 96 : TALL ? 48 : 32;
+    static constexpr int TH = 32;
     static constexpr int AW = TW + 2 * R;
     static constexpr int AH = TH + 2 * R;
     static constexpr int PH = TH + 4 * R;
@@ -125,8 +111,8 @@ struct GeoF {
     static constexpr int NV = RPW + 2 * R;                   // P rows walked per wave
     static constexpr int AHP = SV * RPW;                     // cs rows incl. the last wave's pad rows
     static constexpr int PHP = SV * RPW + 2 * R;             // staged P rows incl. pad rows (>= PH)
-    // S1H segments per A row (6 at 96 rows: an odd SW1 for the bank-spread CS stride)
-    static constexpr int NSEG1 = TALL == 2 ? 6 : NT / AH;
+    // S1H segments per A row
+    static constexpr int NSEG1 = NT / AH;
     static constexpr int SW1 = (AW + NSEG1 - 1) / NSEG1;
     static constexpr int SW2 = (TW + 7) / 8;                 // S2H outputs per thread
     static constexpr int CSS0 = (NSEG1 * SW1 + 2 * R) > 64 ? (NSEG1 * SW1 + 2 * R) : 64;
@@ -146,7 +132,7 @@ struct GeoF {
                AH * (NSEG1 * SW1 > AW ? NSEG1 * SW1 : AW) * 8 + ((PHP * (64 + kBandChunk) + 15) & ~15);
     }
     static constexpr int CSS =
-        (SW1 % 2 == 1 && lds_for(CSS_B) <= (TALL == 2 ? 163840 : R >= 6 ? 81920 : TALL ? 81920 : 53248)) ? CSS_B
+        (SW1 % 2 == 1 && lds_for(CSS_B) <= (R >= 6 ? 81920 : 53248)) ? CSS_B
                                                                                                        : CSS_OLD;
     // mm is two float planes (sum a, sum b), rows of MSA floats.  S2V stores them lane-consecutively
     // (ds_write_addtid_b32, 2 LDS cycles per 64 lanes against 6 for a float2 ds_write_b64); S2H reads
@@ -299,38 +285,24 @@ __device__ __forceinline__ void s2h_load(uint32_t addr, float (&va)[2 * N], floa
 #endif
 template <int R>
 constexpr bool kRolesRight = SM_G_ROLES_RIGHT == 1 || (SM_G_ROLES_RIGHT == 2 && R <= 5 && R != 2);
-// the fused right view on tall tiles too (the radii whose right view runs the wave roles at 3 waves/SIMD)
-#ifndef SM_G_TALL_RIGHT
-#define SM_G_TALL_RIGHT 0
-#endif
-template <int R>
-constexpr bool kGuidedTallRight = SM_G_TALL_RIGHT != 0 && kGuidedTall<R> && kRolesRight<R> && R != 3;
-// the right view's tile kind when tall: SM_G_TALL_RIGHT's value (1: 48 rows, 2: 96 rows)
-constexpr int kTallRightKind = SM_G_TALL_RIGHT;
 template <int R, bool RIGHT>
 constexpr int kGuidedWavesPerEU = (R >= 6 || (RIGHT && (R == 3 || SM_G_ROLES_RIGHT == 1))) ? 2 : 3;
 
-static_assert(GeoF<5, true, 1>::LDS <= 81920, "tall r = 5 tile: two workgroups per CU");
-static_assert(GeoF<5, true, 2>::LDS <= 163840 && GeoF<1, true, 2>::LDS <= 163840, "96-row tile: one workgroup per CU");
+static_assert(GeoF<5, true>::LDS <= 53248 && GeoF<5, false>::LDS <= 53248, "r = 5: three workgroups per CU");
 
 // right-key scale: q * 2^14 in a signed 24-bit field above the 8-bit position field
 constexpr float kRightScale = 16384.0f;
 constexpr float kRightMax = 8388607.0f;    // 2^23 - 1
 constexpr float kRightMin = -8388608.0f;   // -2^23
-// Fused right view's keys (round 4, SM_G_RKEY=1): v_cvt_i32_f32(q * 2^22) with its low 8 bits replaced by
-// the position, i.e. floor(q * 2^14) above the position field.  The conversion saturates at |q| >= 512,
-// which is the old clamp, so a key costs a multiply, one v_min_f32 (a NaN scale, outputs outside the
-// tile or the image, becomes 4e9 and so the largest key), the convert and one v_and_or_b32, instead of
-// v_min_f32 + v_max_f32 + multiply + convert + v_lshl_or_b32 (min / max issue at half rate).
-// SM_G_RKEY=0: the clamped round-3 keys, (int)(q * 2^14) << 8 | position.
-#ifndef SM_G_RKEY
-#define SM_G_RKEY 1
-#endif
-constexpr bool kRkeySat = SM_G_RKEY != 0;
+// Fused right view's keys (round 4): v_cvt_i32_f32(q * 2^22) with its low 8 bits replaced by the position,
+// i.e. floor(q * 2^14) above the position field.  The conversion saturates at |q| >= 512, so a key costs a
+// multiply, one v_min_f32 (a NaN scale, outputs outside the tile or the image, becomes 4e9 and so the
+// largest key), the convert and one v_and_or_b32 (the round-3 clamped (int)(q * 2^14) << 8 | position took
+// v_min_f32 + v_max_f32 + multiply + convert + v_lshl_or_b32: 527.8 -> 515.4 us per 1080p frame).
 constexpr float kRightScaleSat = 4194304.0f;   // 2^22
 
-template <int R, bool RIGHT, int TALL = 0>
-__global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
+template <int R, bool RIGHT>
+__global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fused_kernel(
     const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg, int W, int H, int pitch, int64_t fstride,
     int d_lo, int D, float eps, int valid_mode, uint8_t* __restrict__ disp, int out_pitch, int64_t ostride,
     int tiles_x, int tiles, int* __restrict__ gpart, int K, int* __restrict__ keys) {
@@ -342,7 +314,7 @@ __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesP
     // the v_fmac the f32 form gets: +0.8 % on the left-only kernel, which keeps that form; at r = 2 the
     // right view measured 409.6 -> 417.5 us/frame with it instead of its 5 spilled VGPRs, not kept)
     constexpr bool LEAN = RIGHT && ROLES;
-    using G = GeoF<R, ROLES, TALL>;
+    using G = GeoF<R, ROLES>;
     constexpr int NT = G::NT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* cs = reinterpret_cast<uint32_t*>(smem);                                  // [AHP][CSS] packed sums
@@ -470,7 +442,7 @@ __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesP
         bq[o] = valid_mode == 0 ? 50.0f * (float)(win_count(x, R, W) * win_count(oy, R, H)) : __builtin_huge_valf();
         bdd[o] = -256;
         if constexpr (RIGHT) {
-            rinv[o] = ok ? (kRkeySat ? kRightScaleSat : kRightScale) / (float)(win_count(x, R, W) * win_count(oy, R, H))
+            rinv[o] = ok ? kRightScaleSat / (float)(win_count(x, R, W) * win_count(oy, R, H))
                          : __builtin_nanf("");
             rk[o] = INT_MAX;
         }
@@ -679,18 +651,12 @@ __global__ __launch_bounds__((TALL == 2 ? 768 : TALL ? 384 : kT), (kGuidedWavesP
             bdd[o] = take ? d : bdd[o];
             if constexpr (RIGHT) {
                 // candidate for right pixel u = x - d (slot o): q = (N q) / N, fixed point, position
-                // 7 SW2 + o (the output column relative to this segment, see the file header)
-                int key;
-                if constexpr (kRkeySat) {
-                    // NaN (outputs outside) -> 4e9 -> INT_MAX; the conversion saturates both ways
-                    const float qs = __builtin_fminf(q * rinv[o], 4.0e9f);
-                    int k;
-                    asm("v_cvt_i32_f32 %0, %1" : "=v"(k) : "v"(qs));
-                    key = (k & ~0xFF) | (7 * G::SW2 + o);
-                } else {
-                    const float qs = __builtin_fmaxf(__builtin_fminf(q * rinv[o], kRightMax), kRightMin);
-                    key = ((int)qs << 8) | (7 * G::SW2 + o);
-                }
+                // 7 SW2 + o (the output column relative to this segment, see the file header).
+                // NaN (outputs outside) -> 4e9 -> INT_MAX; the conversion saturates both ways
+                const float qs = __builtin_fminf(q * rinv[o], 4.0e9f);
+                int kq;
+                asm("v_cvt_i32_f32 %0, %1" : "=v"(kq) : "v"(qs));
+                const int key = (kq & ~0xFF) | (7 * G::SW2 + o);
                 rk[o] = key < rk[o] ? key : rk[o];
             }
             sa -= va[o];
@@ -850,16 +816,6 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     constexpr size_t lds_left = (size_t)GeoF<R, kGuidedRoles>::LDS;
     constexpr size_t lds_right = (size_t)GeoF<R, kGuidedRoles && kRolesRight<R>>::LDS;
     if (!gpart) {
-        if constexpr (kGuidedTall<R>) {
-            using GT = GeoF<R, kGuidedRoles, kTallKind>;
-            const int tyt = (H + GT::TH - 1) / GT::TH;
-            const int64_t bt = (int64_t)tiles_x * tyt * batch;
-            if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((guided_fused_kernel<R, false, kTallKind>), dim3((unsigned)bt), dim3(GT::NT),
-                               (size_t)GT::LDS, s, L, Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp,
-                               out_pitch, ostride, tiles_x, tiles_x * tyt, nullptr, 0, keys);
-            return hipGetLastError();
-        }
         hipLaunchKernelGGL((guided_fused_kernel<R, false>), dim3((unsigned)blocks), dim3(kT), lds_left, s, L,
                            Rimg, W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
                            tiles_x * tiles_y, nullptr, 0, keys);
@@ -867,18 +823,6 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
     }
     const int span = 8 * G::SW2;
     const int K = D + span - 1;
-    if constexpr (kGuidedTallRight<R>) {
-        using GT = GeoF<R, kGuidedRoles && kRolesRight<R>, kTallRightKind>;
-        const int tyt = (H + GT::TH - 1) / GT::TH;
-        const int64_t bt = (int64_t)tiles_x * tyt * batch;
-        if (bt > 0x7FFFFFFF) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((guided_fused_kernel<R, true, kTallRightKind>), dim3((unsigned)bt), dim3(GT::NT), (size_t)GT::LDS, s,
-                           L, Rimg, W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x,
-                           tiles_x * tyt, gpart, K, nullptr);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return launch_right_reduce<GT::TH>(gpart, tiles_x, tyt, batch, G::TW, span, K, W, H, right, rpitch, rstride, s);
-    }
     hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), lds_right, s, L, Rimg,
                        W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
                        K, nullptr);
@@ -889,7 +833,7 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
 
 template <int R>
 size_t partial_bytes(int W, int H, int D, int batch) {
-    using G = GeoF<R, false, kGuidedTallRight<R> ? kTallRightKind : 0>;
+    using G = GeoF<R, false>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
 }

@@ -42,10 +42,8 @@ constexpr int kSadBlocks = SM_SAD_BLOCKS;  // K2 blocks per launch (>= 32-row ba
 // rows two neighbouring bands share are read by both at the same phase of their walks (both at the
 // start, or both at the end) while they run side by side on one XCD: the second read hits that XCD's
 // L2.  With every band walking down, band b read its top halo at its start and band b - 1 the same
-// rows at its end, ~12 MB of XCD traffic later (4 MB L2): rocprof counted 1.046x the algorithmic bytes.
-#ifndef SM_SAD_ZIGZAG
-#define SM_SAD_ZIGZAG 1
-#endif
+// rows at its end, ~12 MB of XCD traffic later (4 MB L2): rocprof counted 1.046x the algorithmic bytes
+// (1.004x with the zigzag, at ~3 % of this kernel's time).
 static_assert(kCPT == 4 || kCPT == 8, "K2 columns per thread");
 
 // K2: one column strip x one row band of one d plane per block.  A thread owns kCPT input columns
@@ -75,7 +73,7 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
     if (yo0 >= H) return;                               // block-uniform
     // the walk runs over virtual rows v; image row phys(v) reflects the band's input range
     // [yo0 - R, yo1 + R) (and its output rows [yo0, yo1)) onto itself for a bottom-up band
-    const bool up = SM_SAD_ZIGZAG && (band & 1);
+    const bool up = (band & 1) != 0;
     auto phys = [&](int v) { return up ? yo0 + yo1 - 1 - v : v; };
     const int64_t P = (int64_t)W * H;
     const uint8_t* plane = ad + (int64_t)d * P;

@@ -1535,9 +1535,11 @@ SM_API int sm_last_segment_tree_arrays(sm_handle* h, int* ints, int64_t n_ints, 
     if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
     if (!h->st_valid || h->st.last_P <= 0) return fail(SM_ERR_INVALID_ARG, "no segment-tree call has completed on this handle");
     const int64_t P = h->st.last_P, nlev = h->st.last_nlev, need = 4 * P + nlev + 1;
-    if (!ints || !pdist || n_ints < need || n_bytes < P)
-        return fail(SM_ERR_INVALID_ARG, "buffers too small: %lld ints and %lld bytes needed", (long long)need,
-                    (long long)P);
+    // n_bytes must be the last call's pixel count exactly: a caller slicing the ints by its own width *
+    // height would mis-slice them after a call on another frame shape
+    if (!ints || !pdist || n_ints < need || n_bytes != P)
+        return fail(SM_ERR_INVALID_ARG, "need >= %lld ints and exactly %lld pdist bytes (the last call's pixels)",
+                    (long long)need, (long long)P);
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(hipStreamSynchronize(h->stream));
     SM_HIP(hipMemcpy(ints, h->st.tree_i, (size_t)need * sizeof(int), hipMemcpyDeviceToHost));
@@ -1569,22 +1571,28 @@ SM_API int sm_block_match_bgr_u8(sm_handle* h, const uint8_t* left_bgr, const ui
     uint8_t* dl = h->d_bgr;
     uint8_t* dr = h->d_bgr + row * height;
     const int64_t P = (int64_t)width * height;
-    SM_HIP(hipEventRecord(h->ev[0], s));
+    // the stage split under the same SM_PARAM_STAGE_TIMING rule as the gray host calls
+    const bool ev = h->stage_timing == 1 || (h->stage_timing == 2 && (h->stage_requested || verbose_env()));
+    if (ev) SM_HIP(hipEventRecord(h->ev[0], s));
     SM_HIP(copy2d(dl, row, left_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
     SM_HIP(copy2d(dr, row, right_bgr, pitch, row, height, hipMemcpyHostToDevice, s));
-    SM_HIP(hipEventRecord(h->ev[1], s));
+    if (ev) SM_HIP(hipEventRecord(h->ev[1], s));
     SM_HIP(sm::launch_bgr_to_gray(dl, width, height, (int)row, channels, h->d_left, width, s));
     SM_HIP(sm::launch_bgr_to_gray(dr, width, height, (int)row, channels, h->d_right, width, s));
     rc = run_device(h, h->d_left, h->d_right, width, height, width, 1, P, radius, num_disp, flags, h->d_disp, width, P,
                     nullptr, nullptr, width, P, s);
     if (rc) return rc;
-    SM_HIP(hipEventRecord(h->ev[2], s));
+    if (ev) SM_HIP(hipEventRecord(h->ev[2], s));
     SM_HIP(copy2d(disp_out, out_pitch, h->d_disp, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipEventRecord(h->ev[3], s));
     SM_HIP(hipEventSynchronize(h->ev[3]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
-    SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    if (ev) {
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
+        SM_HIP(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+    } else {
+        h->stage_ms[0] = h->stage_ms[1] = h->stage_ms[2] = 0.f;
+    }
     return SM_OK;
 }
 

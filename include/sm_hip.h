@@ -282,7 +282,9 @@ SM_API int sm_last_segment_tree_stats(sm_handle *h, float *tree_ms, float *total
 /* diagnostics: the last call's last tree (ST-1 its colour tree, ST-2 the colour + depth tree) in BFS
  * order, as SegmentTree.cpp:97-130 lays it out: ints = rank[P] (pixel -> BFS index), parent[P],
  * first[P] (first child), child[P] (count | distance bytes << 8), level offsets[levels + 1]
- * (n_ints >= 4P + levels + 1); pdist[P] = distance byte to the parent.  Synchronous. */
+ * (n_ints >= 4P + levels + 1); pdist[P] = distance byte to the parent, n_bytes == P exactly (the last
+ * call's pixel count; another value is SM_ERR_INVALID_ARG, so a stale width x height cannot mis-slice).
+ * Synchronous. */
 SM_API int sm_last_segment_tree_arrays(sm_handle *h, int *ints, int64_t n_ints, uint8_t *pdist, int64_t n_bytes,
                                        int *levels);
 

@@ -167,3 +167,6 @@ def test_device_bfs_equals_host_bfs(matcher, method):
             assert np.array_equal(got[k], want[k]), (name, k, int((got[k] != want[k]).sum()))
         assert np.array_equal(got_map, want_map), name
         assert matcher.segment_tree_stats()[2] == len(want["lev"]) - 1
+    import gpu_stereo_matching_amd as sm
+    with pytest.raises(sm.SMError):   # a stale frame size is refused, not mis-sliced
+        matcher.segment_tree_arrays(W + 1, H)

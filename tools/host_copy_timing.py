@@ -3,6 +3,7 @@ sys.path.insert(0, os.getcwd())
 import numpy as np
 import gpu_stereo_matching_amd as sm
 m = sm.BlockMatcher(0, 1920, 1080, 256)
+m.set_stage_timing(True)   # the default (auto) records the split only once stage_ms() has been read
 for (W, H, D, r) in ((463, 370, 64, 4), (464, 370, 64, 4), (1920, 1080, 128, 5)):
     L, R = sm.synth_pair(1, W, H, D)
     for _ in range(3): m.match(L, R, r, D)
