@@ -136,10 +136,12 @@ class BlockMatcher:
     def set_guided_eps(self, eps: float):
         _capi.check(self._lib.sm_set_param_f(self._h, _capi.SM_PARAM_GUIDED_EPS, float(eps)))
 
-    def dslice_rehearse(self, left, right, radius: int, num_disp: int, members: int, agg: str = "box") -> np.ndarray:
+    def dslice_rehearse(self, left, right, radius: int, num_disp: int, members: int, agg: str = "box",
+                        lr_check: bool = False) -> np.ndarray:
         """The d-slice split of BlockMatcherGroup.match_dslice with `members` members, run one after
         another on this device (sm_dslice_rehearse_u8): same slice plan, padding and finalisation, with
-        the RCCL MIN reduce-scatter replaced by an elementwise MIN of the members' key maps."""
+        the RCCL MIN reduce-scatter replaced by an elementwise MIN of the members' key maps.  lr_check:
+        the right view's keys take a second MIN and the map is LR-checked (StereoDisparity.cpp:136-147)."""
         if agg not in ("box", "guided"):
             raise ValueError("agg must be 'box' or 'guided'")
         L = _as_u8_image(left, "left")
@@ -149,7 +151,7 @@ class BlockMatcher:
         H, W = L.shape
         out = np.empty((H, W), np.uint8)
         _capi.check(self._lib.sm_dslice_rehearse_u8(self._h, L.ctypes.data, R.ctypes.data, W, H, W, radius, num_disp,
-                                                    _flags(agg, False, False), members, out.ctypes.data, W))
+                                                    _flags(agg, lr_check, False), members, out.ctypes.data, W))
         return out
 
     # -- host-pointer path (blockMatching_gpu replacement) -------------------------------
@@ -467,6 +469,56 @@ class BlockMatcher:
                                                           self._stream_ptr(stream)))
         return keys_t
 
+    def slice_keys_lr_device(self, left_t, right_t, radius: int, d_lo: int, d_hi: int, agg: str = "box",
+                             keys_t=None, right_keys_t=None, stream=None):
+        """Left AND right-view d-slice keys of [d_lo, d_hi) from one fused pass (sm_slice_keys_lr_device): int32
+        [H, W] tensors holding the bit patterns of box uint32 keys (combine with an unsigned MIN) or guided
+        int32 keys (signed MIN).  The right view's key of u is its best (cost << 8 | d) over the slice's d with
+        u + d < W, C_R(u, d) = C_L(u + d, d) (StereoHelper.cpp:156-180)."""
+        import torch
+        if agg not in ("box", "guided"):
+            raise ValueError("agg must be 'box' or 'guided'")
+        H, W = left_t.shape[-2:]
+        if keys_t is None:
+            keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        if right_keys_t is None:
+            right_keys_t = torch.empty((H, W), dtype=torch.int32, device=left_t.device)
+        _check_device_pair(left_t, right_t, keys_t)
+        _check_device_pair(left_t, right_t, right_keys_t)
+        _capi.check(self._lib.sm_slice_keys_lr_device(self._h, left_t.data_ptr(), right_t.data_ptr(), W, H, W, radius,
+                                                      d_lo, d_hi, _flags(agg, False), keys_t.data_ptr(),
+                                                      right_keys_t.data_ptr(), self._stream_ptr(stream)))
+        return keys_t, right_keys_t
+
+    def right_keys_to_disp_device(self, keys_t, out_t=None, stream=None):
+        """Combined right-view keys (any shape, int32) -> dR, the d field of each key (no threshold)."""
+        import torch
+        if keys_t.dtype != torch.int32 or not keys_t.is_contiguous() or not keys_t.is_cuda:
+            raise ValueError("keys_t must be a contiguous int32 device tensor")
+        if out_t is None:
+            out_t = torch.empty(keys_t.shape, dtype=torch.uint8, device=keys_t.device)
+        _check_out(out_t, keys_t.shape, torch.uint8, keys_t.device)
+        _capi.check(self._lib.sm_right_keys_to_disp_device(self._h, keys_t.data_ptr(), keys_t.numel(), out_t.data_ptr(),
+                                                           self._stream_ptr(stream)))
+        return out_t
+
+    def lr_check_device(self, left_disp_t, right_disp_t, out_t=None, mask_t=None, stream=None):
+        """StereoDisparity.cpp:136-147 on [H, W] uint8 device maps: occluded (x - d < 0, d == 0 or
+        |d - dR(x - d)| > 1) -> 0.  out_t may be left_disp_t (in place)."""
+        import torch
+        H, W = left_disp_t.shape
+        for t in (left_disp_t, right_disp_t):
+            _check_out(t, (H, W), torch.uint8, left_disp_t.device, "maps")
+        if out_t is None:
+            out_t = torch.empty_like(left_disp_t)
+        _check_out(out_t, (H, W), torch.uint8, left_disp_t.device)
+        if mask_t is not None:
+            _check_out(mask_t, (H, W), torch.uint8, left_disp_t.device, "mask_t")
+        _capi.check(self._lib.sm_lr_check_device(self._h, left_disp_t.data_ptr(), right_disp_t.data_ptr(), W, H, W,
+                                                 out_t.data_ptr(), mask_t.data_ptr() if mask_t is not None else None,
+                                                 W, self._stream_ptr(stream)))
+        return out_t
+
     def guided_keys_to_disp_device(self, keys_t, out_t=None, stream=None):
         """Combined guided keys -> uint8 disparity (d where q < 50, else 0)."""
         import torch
@@ -544,10 +596,12 @@ class BlockMatcherGroup:
                                                          rd.ctypes.data, mask.ctypes.data, W))
         return out, rd, mask
 
-    def match_dslice(self, left, right, radius: int, num_disp: int, agg: str = "box") -> np.ndarray:
+    def match_dslice(self, left, right, radius: int, num_disp: int, agg: str = "box",
+                     lr_check: bool = False) -> np.ndarray:
         """One frame sharded over disparities (sm_group_dslice_block_match_u8): each member matches
         its slice of [0, num_disp), RCCL MIN reduce-scatter + all-gather over the members' devices.
-        Members must be distinct devices."""
+        lr_check: the right view's slice keys take a second reduce-scatter + all-gather and the map is
+        LR-checked.  Members must be distinct devices."""
         if agg not in ("box", "guided"):
             raise ValueError("agg must be 'box' or 'guided'")
         L = _as_u8_image(left, "left")
@@ -557,7 +611,7 @@ class BlockMatcherGroup:
         H, W = L.shape
         out = np.empty((H, W), np.uint8)
         _capi.check(self._lib.sm_group_dslice_block_match_u8(self._g, L.ctypes.data, R.ctypes.data, W, H, W, radius,
-                                                             num_disp, _flags(agg, False, False), out.ctypes.data, W))
+                                                             num_disp, _flags(agg, lr_check, False), out.ctypes.data, W))
         return out
 
     def match_batch(self, lefts, rights, radius: int, num_disp: int, agg: str = "box", lr_check: bool = False,

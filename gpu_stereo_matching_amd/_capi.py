@@ -43,7 +43,8 @@ EXPORTED = (
     "sm_group_block_match_lr_u8", "sm_group_block_match_batch_u8", "sm_group_dslice_block_match_u8", "sm_guided_slice_keys_device",
     "sm_guided_keys_to_disp_device", "sm_segment_tree_match_bgr_u8", "sm_segment_tree_refined_bgr_u8",
     "sm_last_segment_tree_stats", "sm_last_segment_tree_arrays", "sm_host_alloc", "sm_host_free",
-    "sm_dslice_plan", "sm_dslice_rehearse_u8",
+    "sm_dslice_plan", "sm_dslice_rehearse_u8", "sm_slice_keys_lr_device", "sm_right_keys_to_disp_device",
+    "sm_lr_check_device",
 )
 
 
@@ -124,6 +125,9 @@ def load(path: str = LIB_PATH):
     L.sm_dslice_plan.argtypes = [i64, i, i, i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i64),
                                  ctypes.POINTER(i64)]
     L.sm_dslice_rehearse_u8.argtypes = [vp, vp, vp, i, i, i, i, i, u, i, vp, i]
+    L.sm_slice_keys_lr_device.argtypes = [vp, vp, vp, i, i, i, i, i, i, u, vp, vp, vp]
+    L.sm_right_keys_to_disp_device.argtypes = [vp, vp, i64, vp, vp]
+    L.sm_lr_check_device.argtypes = [vp, vp, vp, i, i, i, vp, vp, i, vp]
     for name in EXPORTED:
         if name not in ("sm_version", "sm_last_error_string"):
             getattr(L, name).restype = ctypes.c_int

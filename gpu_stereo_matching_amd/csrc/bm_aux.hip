@@ -118,7 +118,31 @@ __global__ __launch_bounds__(256) void min_keys_kernel(int* __restrict__ acc, co
     if (i < n) acc[i] = min(acc[i], src[i]);
 }
 
+__global__ __launch_bounds__(256) void min_keys_u32_kernel(uint32_t* __restrict__ acc, const uint32_t* __restrict__ src,
+                                                           int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) acc[i] = min(acc[i], src[i]);
+}
+
+__global__ __launch_bounds__(256) void keys_low_byte_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                            uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint8_t)(keys[i] & 0xFFu);
+}
+
 }  // namespace
+
+hipError_t launch_min_keys_u32(uint32_t* acc, const uint32_t* src, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(min_keys_u32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, src, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_keys_low_byte(const uint32_t* keys, int64_t n, uint8_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(keys_low_byte_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keys, n, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_min_keys(int* acc, const int* src, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;

@@ -366,7 +366,8 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
                 };
                 // RIGHT: klo of output o goes to u_o = x_o - d, khi to u_o - 1 = u_{o-1}; the two
                 // candidates of one u are min'ed in registers, one ds_min_u32 per u
-                uint32_t* rrow = rb + G::rb_row(h * G::HALF + hj) + (obase - d + DMAX + 1);   // + o: u_o
+                // (in slice mode, d_lo > 0, the rows hold u' = u + d_lo: the d_lo = 0 layout of d - d_lo)
+                uint32_t* rrow = rb + G::rb_row(h * G::HALF + hj) + (obase - (d - d_lo) + DMAX + 1);   // + o: u_o
                 uint32_t plo = 0xFFFFFFFFu;
                 if (!dm) {
 #pragma unroll
@@ -472,15 +473,24 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
 // of the four u holds 0xFFFFFFFF or a valid candidate of the others: every entry a tile writes is
 // C_L(u + d, d) of one of its pixels, so a min over a superset of the covering tiles is the same key).
 // The LR check then runs on 4 pixels per thread with dword loads and stores where the rows allow.
+// Slice mode (rkeys != nullptr, multi-GPU d-slices with LR): the partial rows of a pass over d in
+// [d_lo, d_hi) hold u' = u + d_lo (box_match_kernel's right rows), `d_hi` is then the span d_hi - d_lo, and
+// the kernel writes the raw minimum key of every right pixel u to rkeys[f][y][u] (0x7FFFFFFF where no d of
+// the slice has u + d < W) instead of dR: keys of disjoint slices combine with a MIN (below 2^31 at r <= 15,
+// so signed and unsigned agree).
 template <int MAXT>
 __global__ __launch_bounds__(256) void right_reduce_lr_vec_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
                                                                   int tiles_y, int TW, int PWP, int dmax, int d_hi,
                                                                   int W, int H, int check, uint8_t* disp, int opitch,
                                                                   int64_t ostride, uint8_t* __restrict__ right_out,
                                                                   uint8_t* __restrict__ mask_out, int apitch,
-                                                                  int64_t astride) {
+                                                                  int64_t astride, uint32_t* __restrict__ rkeys,
+                                                                  int d_lo) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dr_row[];   // W rounded up to 4
     const int y = blockIdx.x, f = blockIdx.y;
+    uint32_t* krow = rkeys ? rkeys + ((int64_t)f * H + y) * W : nullptr;
+    if (krow)   // right pixels past every slice disparity's reach: u + d_lo >= W
+        for (int u = max(W - d_lo, 0) + (int)threadIdx.x; u < W; u += blockDim.x) krow[u] = 0x7FFFFFFFu;
     const int ty = y / kTileH, j = y - ty * kTileH;
     const uint32_t* base = rpart + (((int64_t)f * tiles_y + ty) * tiles_x * kTileH + j) * PWP;
     const int64_t tstride = (int64_t)kTileH * PWP;
@@ -505,6 +515,13 @@ __global__ __launch_bounds__(256) void right_reduce_lr_vec_kernel(const uint32_t
             k1 = min(k1, v[k].y);
             k2 = min(k2, v[k].z);
             k3 = min(k3, v[k].w);
+        }
+        if (krow) {
+            const uint32_t kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (u + b < W && u + b >= d_lo) krow[u + b - d_lo] = kk[b];
+            continue;
         }
         const uint32_t dr4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(k3, k2, 0x0C0C0400u),
                                                    __builtin_amdgcn_perm(k1, k0, 0x0C0C0400u), 0x05040100u);
@@ -564,6 +581,7 @@ struct RightOut {
     uint8_t* mask;    // optional valid mask
     int pitch;
     int64_t stride;
+    uint32_t* rkeys;  // slice mode: raw right keys [batch][H][W] instead of dR (check 0, right null)
 };
 
 int compute_units() {
@@ -616,9 +634,9 @@ hipError_t launch_rd(const MatchArgs& a, int batch, const RightOut* ro, hipStrea
         // tiles covering one of u .. u + 3: ceil((d_hi + 2) / TW) + 1 at most
         constexpr int kMaxT4 = (DMAX + 2 + G::TW - 1) / G::TW + 1;
         hipLaunchKernelGGL((right_reduce_lr_vec_kernel<kMaxT4>), dim3(a.H, batch), dim3(256),
-                           (size_t)((a.W + 3) & ~3), s, a.rpart, tiles_x, tiles_y, G::TW, G::PWP, DMAX, a.d_hi,
-                           a.W, a.H, ro->check, a.disp, a.out_pitch, a.out_frame_stride, ro->right, ro->mask,
-                           ro->pitch, ro->stride);
+                           (size_t)((a.W + 3) & ~3), s, a.rpart, tiles_x, tiles_y, G::TW, G::PWP, DMAX,
+                           a.d_hi - a.d_lo, a.W, a.H, ro->check, a.disp, a.out_pitch, a.out_frame_stride, ro->right,
+                           ro->mask, ro->pitch, ro->stride, ro->rkeys, a.d_lo);
     } else {
         // no more tiles than CUs (a small frame, batch 1): 16 waves per tile, >= 2 d-pairs each, so every
         // CU runs 16 waves instead of <= 4 (R <= 7: the wide-radius kernels need > 128 VGPRs).  Beyond
@@ -754,10 +772,8 @@ size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch) {
     }
 }
 
-hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,
-                               int aux_pitch, int64_t aux_stride, hipStream_t s) {
-    if (a.d_lo != 0 || a.valid_mode != 0 || !a.disp || !a.rpart || (!check && !right_out)) return hipErrorInvalidValue;
-    const RightOut ro{check, right_out, mask_out, aux_pitch, aux_stride};
+static hipError_t launch_box_right(const MatchArgs& a, int batch, const RightOut* rop, hipStream_t s) {
+    const RightOut& ro = *rop;
     switch (a.radius) {
         case 0: return launch_r<0, true>(a, batch, &ro, s);
         case 1: return launch_r<1, true>(a, batch, &ro, s);
@@ -777,6 +793,21 @@ hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t
         case 15: return launch_r<15, true>(a, batch, &ro, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,
+                               int aux_pitch, int64_t aux_stride, hipStream_t s) {
+    if (a.d_lo != 0 || a.valid_mode != 0 || !a.disp || !a.rpart || (!check && !right_out)) return hipErrorInvalidValue;
+    const RightOut ro{check, right_out, mask_out, aux_pitch, aux_stride, nullptr};
+    return launch_box_right(a, batch, &ro, s);
+}
+
+hipError_t launch_box_slice_lr_keys(const MatchArgs& a, int batch, uint32_t* right_keys, hipStream_t s) {
+    if (a.valid_mode != 0 || !a.keys || !a.rpart || !right_keys || a.d_lo < 0 || a.d_hi <= a.d_lo ||
+        a.d_hi > kMaxDisp)
+        return hipErrorInvalidValue;
+    const RightOut ro{0, nullptr, nullptr, 0, 0, right_keys};
+    return launch_box_right(a, batch, &ro, s);
 }
 
 hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s) {

@@ -48,6 +48,16 @@ hipError_t launch_box_match_generic(const MatchArgs& a, int batch, hipStream_t s
 hipError_t launch_box_match_lr(const MatchArgs& a, int batch, int check, uint8_t* right_out, uint8_t* mask_out,
                                int aux_pitch, int64_t aux_stride, hipStream_t s);
 size_t box_right_partial_bytes(int W, int H, int radius, int D, int batch);
+// d-slice with LR (multi-GPU): one fused pass over d in [a.d_lo, a.d_hi) (radius <= kMaxBoxRadius)
+// writing the left slice keys to a.keys (as launch_box_match) and the right view's slice keys
+// min over d in the slice with u + d < W of (C_L(u + d, d) << 8 | d) to right_keys [batch][H][W]
+// (0x7FFFFFFF where none; every key < 2^31 at these radii): keys of disjoint slices combine with a MIN.  a.rpart:
+// box_right_partial_bytes(W, H, radius, d_hi - d_lo, batch) bytes.
+hipError_t launch_box_slice_lr_keys(const MatchArgs& a, int batch, uint32_t* right_keys, hipStream_t s);
+// acc = min(acc, src) elementwise over n unsigned keys
+hipError_t launch_min_keys_u32(uint32_t* acc, const uint32_t* src, int64_t n, hipStream_t s);
+// right-view key map -> dR: the d field (low byte) of each key, no threshold (StereoHelper.cpp:131-154)
+hipError_t launch_keys_low_byte(const uint32_t* keys, int64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_keys_to_disp(const uint32_t* keys, int W, int H, uint32_t thresh_key,
                                uint8_t* disp, int out_pitch, hipStream_t s);
 // acc = min(acc, src) elementwise over n signed keys (the d-slice MIN, rehearsed on one device)

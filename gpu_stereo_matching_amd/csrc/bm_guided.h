@@ -28,6 +28,13 @@ size_t guided_right_partial_bytes(int W, int H, int radius, int D, int batch);
 hipError_t launch_guided_slice_keys(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                                     int64_t frame_stride, int radius, int d_lo, int d_hi, float eps, int* keys,
                                     hipStream_t s);
+// The same slice pass with the fused right view (LR over d-slices): also the right view's slice keys
+// (cost field of q_R = q_L(u + d, d), 2^-14 fixed point) | d for the best d in the slice with u + d < W
+// (StereoHelper.cpp:156-180; INT_MAX where none), [batch][H][W] int32, combined with a signed min.
+// gpart: guided_right_partial_bytes(W, H, radius, d_hi - d_lo, batch) bytes.
+hipError_t launch_guided_slice_lr_keys(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                       int64_t frame_stride, int radius, int d_lo, int d_hi, float eps, int* keys,
+                                       int* right_keys, int* gpart, hipStream_t s);
 // combined keys -> disparity with the Device.cu:37 threshold q < 50
 hipError_t launch_guided_keys_to_disp(const int* keys, int W, int H, uint8_t* disp, int out_pitch, hipStream_t s);
 

@@ -459,7 +459,8 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             // row_shr:1 = lane - 1, i.e. the previous segment of the same row (lane 8r + s)
             const int in = __builtin_amdgcn_update_dpp(INT_MAX, leaving, 0x111, 0xF, 0xF, false) - G::SW2;
             rk[0] = seg_first ? INT_MAX : in;
-            if (seg_last) gdst[(int64_t)k * G::TH] = leaving;
+            // step k - d_lo: a slice pass (d_lo > 0) lays its chain out as the d_lo = 0 pass of d - d_lo does
+            if (seg_last) gdst[(int64_t)(k - d_lo) * G::TH] = leaving;
         }
     };
 
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     }
     // drain the right-key chain: 8 SW2 - 1 more steps move every slot out through the last segment
     if constexpr (RIGHT) {
-        for (int k = D; k < K; ++k) chain_step(k);
+        for (int k = D; k < d_lo + K; ++k) chain_step(k);
     }
     if (valid_mode == 2) {
         // d-slice keys: (q * 2^14 << 8) | d, INT_MAX where no d of the slice is valid
@@ -740,15 +741,20 @@ __global__ __launch_bounds__(256) void guided_keys_to_disp_kernel(const int* __r
 // MAXT >= the most tiles covering one u, (K + TW - 1) / TW + 1: a fixed trip count, so every key load of
 // an entry issues before the first compare (round 4; the loop over the covering tiles had each load wait
 // for the compare before it)
+// Slice mode (rkeys != nullptr, multi-GPU d-slices with LR): the chains of a pass over d in [d_lo, d_hi)
+// index u' = u + d_lo (the layout of the d_lo = 0 pass of d - d_lo), and the kernel writes the right key
+// of every pixel u, (its cost field) | d, to rkeys[f][y][u] (INT_MAX where no d of the slice has u + d < W):
+// keys of disjoint slices combine with a signed MIN (smaller cost, then smaller d).
 template <int TH, int MAXT>
 __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __restrict__ gpart, int tiles_x, int tiles,
                                                                   int TW, int SPAN, int K, int W, int H,
                                                                   uint8_t* __restrict__ right, int rpitch,
-                                                                  int64_t rstride) {
+                                                                  int64_t rstride, int* __restrict__ rkeys, int d_lo) {
     constexpr int UC = 64;
     __shared__ uint8_t band[TH][UC];
     const int u0 = blockIdx.x * UC, ty = blockIdx.y, f = blockIdx.z;
     const int* base = gpart + ((int64_t)f * tiles + (int64_t)ty * tiles_x) * K * TH;
+    int* kf = rkeys ? rkeys + (int64_t)f * H * W : nullptr;
     for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
         const int j = e % TH, ul = e / TH, u = u0 + ul;
         int dr = 0;
@@ -773,9 +779,17 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
                 }
             }
             dr = (tlo + bm) * TW + (best & 0xFF) - u;
+            const int y = ty * TH + j;
+            if (kf && y < H && u >= d_lo) kf[(int64_t)y * W + u - d_lo] = (best & ~0xFF) | (dr + d_lo);
+        }
+        if (kf) {   // right pixels with u + d_lo >= W: no d of the slice reaches them
+            const int y = ty * TH + j;
+            if (y < H && u < W && u >= W - d_lo) kf[(int64_t)y * W + u] = INT_MAX;
+            continue;
         }
         band[j][ul] = (uint8_t)dr;
     }
+    if (kf) return;
     __syncthreads();
     uint8_t* Rf = right + (int64_t)f * rstride;
     for (int e = threadIdx.x; e < TH * UC; e += blockDim.x) {
@@ -788,13 +802,14 @@ __global__ __launch_bounds__(256) void guided_right_reduce_kernel(const int* __r
 // the reduce with the smallest instantiated MAXT >= (K + TW - 1) / TW + 1 (D <= 256, TW >= 36: <= 10)
 template <int TH>
 hipError_t launch_right_reduce(const int* gpart, int tiles_x, int tiles_y, int batch, int TW, int span, int K, int W,
-                               int H, uint8_t* right, int rpitch, int64_t rstride, hipStream_t s) {
+                               int H, uint8_t* right, int rpitch, int64_t rstride, int* rkeys, int d_lo,
+                               hipStream_t s) {
     const int need = (K + TW - 1) / TW + 1;
     const dim3 grid((unsigned)((W + 63) / 64), (unsigned)tiles_y, (unsigned)batch);
     const int tiles = tiles_x * tiles_y;
 #define SM_RIGHT_REDUCE(M)                                                                                      \
     hipLaunchKernelGGL((guided_right_reduce_kernel<TH, M>), grid, dim3(256), 0, s, gpart, tiles_x, tiles, TW, span, K, \
-                       W, H, right, rpitch, rstride)
+                       W, H, right, rpitch, rstride, rkeys, d_lo)
     if (need <= 4) SM_RIGHT_REDUCE(4);
     else if (need <= 6) SM_RIGHT_REDUCE(6);
     else if (need <= 8) SM_RIGHT_REDUCE(8);
@@ -807,7 +822,8 @@ hipError_t launch_right_reduce(const int* gpart, int tiles_x, int tiles_y, int b
 template <int R>
 hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pitch, int64_t fstride, int batch,
                      int d_lo, int D, float eps, int valid_mode, uint8_t* disp, int out_pitch, int64_t ostride,
-                     int* gpart, uint8_t* right, int rpitch, int64_t rstride, int* keys, hipStream_t s) {
+                     int* gpart, uint8_t* right, int rpitch, int64_t rstride, int* keys, hipStream_t s,
+                     int* rkeys = nullptr) {
     using G = GeoF<R, false>;   // tile geometry (TW, TH, SW2) is the same with or without the roles
     const int tiles_x = (W + G::TW - 1) / G::TW, tiles_y = (H + G::TH - 1) / G::TH;
     const int64_t blocks = (int64_t)tiles_x * tiles_y * batch;
@@ -821,18 +837,21 @@ hipError_t run_fused(const uint8_t* L, const uint8_t* Rimg, int W, int H, int pi
                            tiles_x * tiles_y, nullptr, 0, keys);
         return hipGetLastError();
     }
+    // with the right view: valid_mode 0 (d_lo 0, the left map + dR) or 2 (a d slice: left keys + right keys in
+    // rkeys, the chains laid out for d - d_lo)
     const int span = 8 * G::SW2;
-    const int K = D + span - 1;
+    const int K = (D - d_lo) + span - 1;
     hipLaunchKernelGGL((guided_fused_kernel<R, true>), dim3((unsigned)blocks), dim3(kT), lds_right, s, L, Rimg,
-                       W, H, pitch, fstride, 0, D, eps, 0, disp, out_pitch, ostride, tiles_x, tiles_x * tiles_y, gpart,
-                       K, nullptr);
+                       W, H, pitch, fstride, d_lo, D, eps, valid_mode, disp, out_pitch, ostride, tiles_x,
+                       tiles_x * tiles_y, gpart, K, keys);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_right_reduce<G::TH>(gpart, tiles_x, tiles_y, batch, G::TW, span, K, W, H, right, rpitch, rstride, s);
+    return launch_right_reduce<G::TH>(gpart, tiles_x, tiles_y, batch, G::TW, span, K, W, H, right, rpitch, rstride,
+                                      rkeys, d_lo, s);
 }
 
 template <int R>
-size_t partial_bytes(int W, int H, int D, int batch) {
+size_t partial_bytes(int W, int H, int D, int batch) {   // D: the pass's span d_hi - d_lo
     using G = GeoF<R, false>;
     const int64_t tiles = (int64_t)((W + G::TW - 1) / G::TW) * ((H + G::TH - 1) / G::TH);
     return (size_t)(tiles * batch * (D + 8 * G::SW2 - 1) * G::TH * 4);
@@ -904,6 +923,26 @@ hipError_t launch_guided_slice_keys(const uint8_t* L, const uint8_t* R, int W, i
         default: return hipErrorInvalidValue;
     }
 #undef SM_GUIDED_SLICE
+}
+
+hipError_t launch_guided_slice_lr_keys(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
+                                       int64_t frame_stride, int radius, int d_lo, int d_hi, float eps, int* keys,
+                                       int* right_keys, int* gpart, hipStream_t s) {
+    if (d_lo < 0 || d_hi <= d_lo || d_hi > kMaxDisp || !keys || !right_keys || !gpart) return hipErrorInvalidValue;
+#define SM_GUIDED_SLICE_LR(r) \
+    case r: return run_fused<r>(L, R, W, H, pitch, frame_stride, batch, d_lo, d_hi, eps, 2, nullptr, 0, 0, gpart, nullptr, 0, 0, keys, s, right_keys)
+    switch (radius) {
+        SM_GUIDED_SLICE_LR(0);
+        SM_GUIDED_SLICE_LR(1);
+        SM_GUIDED_SLICE_LR(2);
+        SM_GUIDED_SLICE_LR(3);
+        SM_GUIDED_SLICE_LR(4);
+        SM_GUIDED_SLICE_LR(5);
+        SM_GUIDED_SLICE_LR(6);
+        SM_GUIDED_SLICE_LR(7);
+        default: return hipErrorInvalidValue;
+    }
+#undef SM_GUIDED_SLICE_LR
 }
 
 hipError_t launch_guided_keys_to_disp(const int* keys, int W, int H, uint8_t* disp, int out_pitch, hipStream_t s) {

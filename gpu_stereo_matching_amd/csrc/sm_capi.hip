@@ -699,6 +699,17 @@ DslicePlan dslice_plan(int64_t P, int D, int n, int k, int H = 1) {
 
 // keys no d of the slice improves: the Device.cu:37 seed (box) / INT32_MAX (guided, signed keys)
 uint32_t dslice_none_key(int radius, bool guided) { return guided ? 0x7FFFFFFFu : seed_key(radius); }
+// right-view keys no d of the slice reaches (no seed: StereoHelper.cpp:131-154 has no threshold); box right
+// keys are < 2^31 at the fused right view's radii (255 * 31^2 << 8), so one value serves both MINs
+uint32_t dslice_none_rkey(bool) { return 0x7FFFFFFFu; }
+
+// One d-sliced frame: geometry, aggregation and whether the LR check runs (SM_LR_CHECK: a second key map
+// for the right view, C_R(u, d) = C_L(u + d, d), reduced with its own MIN; StereoHelper.cpp:156-180)
+struct DsliceCfg {
+    int W, H, radius, D;
+    bool guided, lr;
+    int64_t P() const { return (int64_t)W * H; }
+};
 
 int ensure_dsl(sm_handle* h, size_t need) {
     if (h->dsl_bytes >= need) return SM_OK;
@@ -719,20 +730,23 @@ bool dslice_fault(int k, const char* phase) {
     return colon && atoi(e) == k && strcmp(colon + 1, phase) == 0;
 }
 
-// Member-side key pass over its slice: keys[0, padded) on stream s from the frames already on the
-// device (dL / dR, pitch W).
-int dslice_keys(sm_handle* h, const DslicePlan& p, const uint8_t* dL, const uint8_t* dR, int W, int H, int radius,
-                bool guided, uint32_t* keys, hipStream_t s) {
+// The slice pass over [d_lo, d_hi) of frames already on the device (pitch `pitch`): left keys, and with
+// `rkeys` the right view's keys from the same fused pass (its per-tile partials in the handle's rpart
+// workspace).  Keys are [H][W]; no padding.
+int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, int H, int pitch, int radius, int d_lo,
+                    int d_hi, bool guided, uint32_t* keys, uint32_t* rkeys, hipStream_t s) {
     const int64_t P = (int64_t)W * H;
-    const uint32_t none = dslice_none_key(radius, guided);
-    if (p.padded > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(p.padded - P), s));
-    if (p.hi <= p.lo) {   // more members than disparities: an empty slice contributes "no match"
-        SM_HIP(hipMemsetD32Async(keys, (int)none, (size_t)P, s));
-        return SM_OK;
-    }
     if (guided) {
-        SM_HIP(sm::launch_guided_slice_keys(dL, dR, W, H, W, 1, P, radius, p.lo, p.hi, h->guided_eps,
-                                            reinterpret_cast<int*>(keys), s));
+        if (!rkeys) {
+            SM_HIP(sm::launch_guided_slice_keys(dL, dR, W, H, pitch, 1, P, radius, d_lo, d_hi, h->guided_eps,
+                                                reinterpret_cast<int*>(keys), s));
+            return SM_OK;
+        }
+        int rc = ensure_rpart(h, sm::guided_right_partial_bytes(W, H, radius, d_hi - d_lo, 1));
+        if (rc) return rc;
+        SM_HIP(sm::launch_guided_slice_lr_keys(dL, dR, W, H, pitch, 1, P, radius, d_lo, d_hi, h->guided_eps,
+                                               reinterpret_cast<int*>(keys), reinterpret_cast<int*>(rkeys),
+                                               reinterpret_cast<int*>(h->d_rpart), s));
         return SM_OK;
     }
     sm::MatchArgs a{};
@@ -740,20 +754,43 @@ int dslice_keys(sm_handle* h, const DslicePlan& p, const uint8_t* dL, const uint
     a.right = dR;
     a.W = W;
     a.H = H;
-    a.pitch = W;
+    a.pitch = pitch;
     a.frame_stride = P;
     a.radius = radius;
-    a.d_lo = p.lo;
-    a.d_hi = p.hi;
+    a.d_lo = d_lo;
+    a.d_hi = d_hi;
     a.valid_mode = 0;
     a.seed_key = seed_key(radius);
     a.thresh_key = seed_key(radius);
     a.keys = keys;
-    SM_HIP(sm::launch_box_match(a, 1, s));
+    if (!rkeys) {
+        SM_HIP(sm::launch_box_match(a, 1, s));
+        return SM_OK;
+    }
+    int rc = ensure_rpart(h, sm::box_right_partial_bytes(W, H, radius, d_hi - d_lo, 1));
+    if (rc) return rc;
+    a.rpart = h->d_rpart;
+    SM_HIP(sm::launch_box_slice_lr_keys(a, 1, rkeys, s));
     return SM_OK;
 }
 
-// A reduced key chunk -> uint8 (the Device.cu:37 threshold, after the MIN)
+// Member-side key pass over its slice: keys[0, padded) (and rkeys with LR) on stream s from the frames
+// already on the device (dL / dR, pitch W).
+int dslice_keys(sm_handle* h, const DslicePlan& p, const DsliceCfg& c, const uint8_t* dL, const uint8_t* dR,
+                uint32_t* keys, uint32_t* rkeys, hipStream_t s) {
+    const int64_t P = c.P();
+    const uint32_t none = dslice_none_key(c.radius, c.guided), rnone = dslice_none_rkey(c.guided);
+    if (p.padded > P) SM_HIP(hipMemsetD32Async(keys + P, (int)none, (size_t)(p.padded - P), s));
+    if (rkeys && p.padded > P) SM_HIP(hipMemsetD32Async(rkeys + P, (int)rnone, (size_t)(p.padded - P), s));
+    if (p.hi <= p.lo) {   // more members than disparities: an empty slice contributes "no match"
+        SM_HIP(hipMemsetD32Async(keys, (int)none, (size_t)P, s));
+        if (rkeys) SM_HIP(hipMemsetD32Async(rkeys, (int)rnone, (size_t)P, s));
+        return SM_OK;
+    }
+    return slice_keys_pass(h, dL, dR, c.W, c.H, c.W, c.radius, p.lo, p.hi, c.guided, keys, rkeys, s);
+}
+
+// A reduced key chunk -> uint8 (the Device.cu:37 threshold, after the MIN); a right-view chunk -> its d field
 int dslice_finalise(const uint32_t* mine, int64_t chunk, int radius, bool guided, uint8_t* mine8, hipStream_t s) {
     if (guided)
         SM_HIP(sm::launch_guided_keys_to_disp(reinterpret_cast<const int*>(mine), (int)chunk, 1, mine8, (int)chunk, s));
@@ -763,7 +800,9 @@ int dslice_finalise(const uint32_t* mine, int64_t chunk, int radius, bool guided
 }
 
 // Member workspace: keys [padded] | reduced chunk [chunk] | uint8 chunk [chunk] | gathered map [padded] |
-// gathered left frame [n * rows_per * W] | gathered right frame [same]  (each region 256-B aligned)
+// gathered left frame [n * rows_per * W] | gathered right frame [same] | with LR the right view's
+// keys [padded] | reduced chunk [chunk] | uint8 chunk [chunk] | gathered right map [padded]
+// (each region 256-B aligned)
 struct DsliceWs {
     uint32_t* keys;
     uint32_t* mine;
@@ -771,11 +810,15 @@ struct DsliceWs {
     uint8_t* map;
     uint8_t* gl;
     uint8_t* gr;
+    uint32_t* rkeys;
+    uint32_t* rmine;
+    uint8_t* rmine8;
+    uint8_t* rmap;
     int64_t slot;   // bytes of one member's row slot (rows_per * W)
     size_t bytes;
 };
 inline int64_t a256(int64_t v) { return (v + 255) & ~(int64_t)255; }
-DsliceWs dslice_ws(uint8_t* base, const DslicePlan& p, int n, int W) {
+DsliceWs dslice_ws(uint8_t* base, const DslicePlan& p, int n, int W, bool lr) {
     DsliceWs w;
     w.slot = (int64_t)p.rows_per * W;
     int64_t o = 0;
@@ -791,6 +834,18 @@ DsliceWs dslice_ws(uint8_t* base, const DslicePlan& p, int n, int W) {
     o += a256(n * w.slot);
     w.gr = base + o;
     o += a256(n * w.slot);
+    w.rkeys = w.rmine = nullptr;
+    w.rmine8 = w.rmap = nullptr;
+    if (lr) {
+        w.rkeys = reinterpret_cast<uint32_t*>(base + o);
+        o += a256(p.padded * 4);
+        w.rmine = reinterpret_cast<uint32_t*>(base + o);
+        o += a256(p.chunk * 4);
+        w.rmine8 = base + o;
+        o += a256(p.chunk);
+        w.rmap = base + o;
+        o += a256(p.padded);
+    }
     w.bytes = (size_t)o;
     return w;
 }
@@ -809,17 +864,21 @@ int dslice_upload_rows(const DslicePlan& p, const DsliceWs& w, int k, const uint
 // Phase 1 of member k (its worker thread): workspace and the upload of its rows, then a stream sync
 // so that every local failure (allocation, copy) is known before any member enqueues a collective.  A
 // member that fails here returns before phase 2 starts, so nobody waits on it.
-int dslice_member_upload(sm_handle* h, int k, int n, const uint8_t* left, const uint8_t* right, int W, int H,
-                         int pitch, int D) {
-    const int64_t P = (int64_t)W * H;
-    const DslicePlan p = dslice_plan(P, D, n, k, H);
+int dslice_member_upload(sm_handle* h, int k, int n, const uint8_t* left, const uint8_t* right, const DsliceCfg& c,
+                         int pitch) {
+    const DslicePlan p = dslice_plan(c.P(), c.D, n, k, c.H);
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
     if (dslice_fault(k, "keys")) return fail(SM_ERR_LAUNCH, "d-slice member %d: injected fault (keys)", k);
-    int rc = ensure_dsl(h, dslice_ws(nullptr, p, n, W).bytes);
+    int rc = ensure_dsl(h, dslice_ws(nullptr, p, n, c.W, c.lr).bytes);
     if (rc) return rc;
-    const DsliceWs w = dslice_ws(h->d_dsl, p, n, W);
-    rc = dslice_upload_rows(p, w, k, left, right, W, pitch, s);
+    if (c.lr && p.hi > p.lo) {   // the right view's per-tile partials, before any collective
+        rc = ensure_rpart(h, c.guided ? sm::guided_right_partial_bytes(c.W, c.H, c.radius, p.hi - p.lo, 1)
+                                      : sm::box_right_partial_bytes(c.W, c.H, c.radius, p.hi - p.lo, 1));
+        if (rc) return rc;
+    }
+    const DsliceWs w = dslice_ws(h->d_dsl, p, n, c.W, c.lr);
+    rc = dslice_upload_rows(p, w, k, left, right, c.W, pitch, s);
     if (rc) return rc;
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;
@@ -832,15 +891,16 @@ struct DsliceSync {
 };
 
 // Phase 2 of member k: in-place all-gathers of the pair's row slots, the slice keys, MIN reduce-scatter,
-// finalise, all-gather of the map, member 0 downloads.  Waits by polling its stream and the shared abort
-// flag (and RCCL's async error), so that no member blocks forever on a collective a failed peer never
-// joined (the ncclCommAbort pattern).  On any failure the member's communicator is aborted and its slot
-// set to null (the group re-creates them).
-int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, DsliceSync* sync, int k, int n, int W,
-                          int H, int radius, int D, bool guided, uint8_t* disp_out, int out_pitch) {
-    const int64_t P = (int64_t)W * H;
-    const DslicePlan p = dslice_plan(P, D, n, k, H);
-    const DsliceWs w = dslice_ws(h->d_dsl, p, n, W);
+// finalise, all-gather of the map, member 0 downloads.  With LR the right view's keys take the same
+// reduce-scatter / finalise (their d field) / all-gather, and member 0 applies StereoDisparity.cpp:136-147
+// to the gathered maps before the download.  Waits by polling its stream and the shared abort flag (and
+// RCCL's async error), so that no member blocks forever on a collective a failed peer never joined (the
+// ncclCommAbort pattern).  On any failure the member's communicator is aborted and its slot set to null
+// (the group re-creates them).
+int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, DsliceSync* sync, int k, int n,
+                          const DsliceCfg& c, uint8_t* disp_out, int out_pitch) {
+    const DslicePlan p = dslice_plan(c.P(), c.D, n, k, c.H);
+    const DsliceWs w = dslice_ws(h->d_dsl, p, n, c.W, c.lr);
     hipStream_t s = h->stream;
     // every failure of phase 2 goes through bail, so the others stop polling for this member
     auto bail = [&](int code, const char* what) {
@@ -855,14 +915,24 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
     if (api->all_gather(w.gl + k * w.slot, w.gl, (size_t)w.slot, ncclUint8, *comm, s) != ncclSuccess ||
         api->all_gather(w.gr + k * w.slot, w.gr, (size_t)w.slot, ncclUint8, *comm, s) != ncclSuccess)
         return bail(SM_ERR_LAUNCH, "ncclAllGather (pair rows) failed");
-    if (dslice_keys(h, p, w.gl, w.gr, W, H, radius, guided, w.keys, s)) return bail(SM_ERR_LAUNCH, "slice keys launch failed");
-    // box keys (SAD << 8 | d) are < 2^31 and compare the same signed or unsigned; guided keys are signed
-    if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, guided ? ncclInt32 : ncclUint32, ncclMin, *comm, s) !=
-        ncclSuccess)
+    if (dslice_keys(h, p, c, w.gl, w.gr, w.keys, w.rkeys, s)) return bail(SM_ERR_LAUNCH, "slice keys launch failed");
+    // box keys (SAD << 8 | d) compare as unsigned (the right view's too); guided keys are signed
+    const ncclDataType_t kt = c.guided ? ncclInt32 : ncclUint32;
+    if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, kt, ncclMin, *comm, s) != ncclSuccess)
         return bail(SM_ERR_LAUNCH, "ncclReduceScatter failed");
-    if (dslice_finalise(w.mine, p.chunk, radius, guided, w.mine8, s)) return bail(SM_ERR_LAUNCH, "finalise launch failed");
+    if (c.lr && api->reduce_scatter(w.rkeys, w.rmine, (size_t)p.chunk, kt, ncclMin, *comm, s) != ncclSuccess)
+        return bail(SM_ERR_LAUNCH, "ncclReduceScatter (right keys) failed");
+    if (dslice_finalise(w.mine, p.chunk, c.radius, c.guided, w.mine8, s) ||
+        (c.lr && sm::launch_keys_low_byte(w.rmine, p.chunk, w.rmine8, s) != hipSuccess))
+        return bail(SM_ERR_LAUNCH, "finalise launch failed");
     if (api->all_gather(w.mine8, w.map, (size_t)p.chunk, ncclUint8, *comm, s) != ncclSuccess)
         return bail(SM_ERR_LAUNCH, "ncclAllGather failed");
+    if (c.lr && api->all_gather(w.rmine8, w.rmap, (size_t)p.chunk, ncclUint8, *comm, s) != ncclSuccess)
+        return bail(SM_ERR_LAUNCH, "ncclAllGather (right map) failed");
+    if (c.lr && k == 0 &&
+        sm::launch_lr_check(w.map, c.W, c.P(), w.rmap, c.W, c.P(), 0, c.W, c.H, 1, w.map, c.W, c.P(), nullptr, nullptr,
+                            c.W, c.P(), s) != hipSuccess)
+        return bail(SM_ERR_LAUNCH, "LR check launch failed");
     for (;;) {
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) break;
@@ -874,7 +944,7 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
         std::this_thread::yield();
     }
     if (k == 0) {
-        const hipError_t e = copy2d(disp_out, out_pitch, w.map, W, W, H, hipMemcpyDeviceToHost, s);
+        const hipError_t e = copy2d(disp_out, out_pitch, w.map, c.W, c.W, c.H, hipMemcpyDeviceToHost, s);
         if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return bail(SM_ERR_LAUNCH, "map download failed");
     }
     return SM_OK;
@@ -1170,6 +1240,56 @@ SM_API int sm_guided_keys_to_disp_device(sm_handle* h, const int32_t* d_keys, in
         return fail(SM_ERR_INVALID_ARG, "bad guided_keys_to_disp arguments");
     SM_HIP(hipSetDevice(h->device));
     SM_HIP(sm::launch_guided_keys_to_disp(d_keys, width, height, d_disp, out_pitch, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_slice_keys_lr_device(sm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                                   int pitch, int radius, int d_lo, int d_hi, unsigned flags, void* d_left_keys,
+                                   void* d_right_keys, void* stream) {
+    int rc = check_geometry(h, width, height, pitch, radius, d_hi > 0 ? d_hi : 1);
+    if (rc) return rc;
+    if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
+        return fail(SM_ERR_INVALID_ARG, "slice LR keys: flags 0x%x (SM_AGG_BOX or SM_AGG_GUIDED)", flags);
+    const bool guided = (flags & SM_AGG_GUIDED) != 0;
+    if (radius > (guided ? sm::kMaxFastRadius : sm::kMaxBoxRadius))
+        return fail(SM_ERR_INVALID_ARG, "slice LR keys: radius %d > %d", radius,
+                    guided ? sm::kMaxFastRadius : sm::kMaxBoxRadius);
+    if (d_lo < 0 || d_hi <= d_lo || d_hi > sm::kMaxDisp)
+        return fail(SM_ERR_INVALID_ARG, "bad slice [%d,%d)", d_lo, d_hi);
+    if (!d_left || !d_right || !d_left_keys || !d_right_keys) return fail(SM_ERR_INVALID_ARG, "null device pointer");
+    if ((int64_t)width * height > (int64_t)h->max_w * h->max_h)
+        return fail(SM_ERR_CAPACITY, "frame %dx%d exceeds handle capacity", width, height);
+    SM_HIP(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    // the right view's per-tile partials live in the handle's workspace: ordered after the handle's last
+    // workspace pass on another stream, as run_device orders its passes
+    if (h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    rc = slice_keys_pass(h, d_left, d_right, width, height, pitch, radius, d_lo, d_hi, guided,
+                         static_cast<uint32_t*>(d_left_keys), static_cast<uint32_t*>(d_right_keys), s);
+    SM_HIP(hipEventRecord(h->scratch_ev, s));
+    h->scratch_stream = s;
+    h->scratch_pending = true;
+    return rc;
+}
+
+SM_API int sm_right_keys_to_disp_device(sm_handle* h, const void* d_keys, int64_t n, uint8_t* d_disp, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_keys || !d_disp || n < 0) return fail(SM_ERR_INVALID_ARG, "bad right_keys_to_disp arguments");
+    SM_HIP(hipSetDevice(h->device));
+    SM_HIP(sm::launch_keys_low_byte(static_cast<const uint32_t*>(d_keys), n, d_disp, (hipStream_t)stream));
+    return SM_OK;
+}
+
+SM_API int sm_lr_check_device(sm_handle* h, const uint8_t* d_left_disp, const uint8_t* d_right_disp, int width,
+                              int height, int pitch, uint8_t* d_out, uint8_t* d_mask, int out_pitch, void* stream) {
+    if (!h) return fail(SM_ERR_INVALID_ARG, "null handle");
+    if (!d_left_disp || !d_right_disp || !d_out || width <= 0 || height <= 0 || pitch < width || out_pitch < width)
+        return fail(SM_ERR_INVALID_ARG, "bad lr_check arguments");
+    if (d_right_disp == d_out) return fail(SM_ERR_INVALID_ARG, "lr_check: the right map cannot be the output");
+    SM_HIP(hipSetDevice(h->device));
+    const int64_t P = (int64_t)width * height;
+    SM_HIP(sm::launch_lr_check(d_left_disp, pitch, P, d_right_disp, pitch, P, 0, width, height, 1, d_out, out_pitch, P,
+                               nullptr, d_mask, out_pitch, P, (hipStream_t)stream));
     return SM_OK;
 }
 
@@ -1700,10 +1820,14 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
     if (width <= 0 || height <= 0 || pitch < width || out_pitch < width)
         return fail(SM_ERR_INVALID_ARG, "bad frame geometry %dx%d pitch %d out_pitch %d", width, height, pitch,
                     out_pitch);
-    if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
-        return fail(SM_ERR_INVALID_ARG, "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED only; no LR, median, staged)",
-                    flags);
+    if ((flags & ~(unsigned)(SM_AGG_GUIDED | SM_LR_CHECK)) != 0u)
+        return fail(SM_ERR_INVALID_ARG,
+                    "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED, optionally SM_LR_CHECK; no median, staged)", flags);
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
+    const DsliceCfg cfg{width, height, radius, num_disp, guided, (flags & SM_LR_CHECK) != 0};
+    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius)
+        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d (the fused right view)", radius,
+                    sm::kMaxBoxRadius);
     for (GroupWorker* w : g->w) {
         int rc = check_geometry(w->h, width, height, width, radius, num_disp);
         if (rc) return rc;
@@ -1719,9 +1843,7 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
     std::vector<std::function<int()>> jobs;
     for (int k = 0; k < n; ++k) {
         sm_handle* h = g->w[k]->h;
-        jobs.push_back([=]() -> int {
-            return dslice_member_upload(h, k, n, left, right, width, height, pitch, num_disp);
-        });
+        jobs.push_back([=]() -> int { return dslice_member_upload(h, k, n, left, right, cfg, pitch); });
     }
     rc = group_run(g, jobs);
     if (rc) return rc;
@@ -1733,10 +1855,7 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
         sm_handle* h = g->w[k]->h;
         ncclComm_t* c = &g->comms[k];
         DsliceSync* sy = &sync;
-        jobs.push_back([=]() -> int {
-            return dslice_member_collect(h, api, c, sy, k, n, width, height, radius, num_disp, guided, disp_out,
-                                         out_pitch);
-        });
+        jobs.push_back([=]() -> int { return dslice_member_collect(h, api, c, sy, k, n, cfg, disp_out, out_pitch); });
     }
     rc = group_run(g, jobs);
     if (sync.abort.load()) {   // some communicators were aborted: drop the rest, re-create on next use
@@ -1768,26 +1887,35 @@ SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_
     if (!left || !right || !disp_out) return fail(SM_ERR_INVALID_ARG, "null image pointer");
     if (out_pitch < width) return fail(SM_ERR_INVALID_ARG, "out_pitch %d < width %d", out_pitch, width);
     if (members < 1 || members > 64) return fail(SM_ERR_INVALID_ARG, "members %d out of [1, 64]", members);
-    if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
-        return fail(SM_ERR_INVALID_ARG, "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED only)", flags);
+    if ((flags & ~(unsigned)(SM_AGG_GUIDED | SM_LR_CHECK)) != 0u)
+        return fail(SM_ERR_INVALID_ARG, "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED, optionally SM_LR_CHECK)",
+                    flags);
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
     if (guided && radius > sm::kMaxFastRadius)
         return fail(SM_ERR_INVALID_ARG, "guided aggregation: radius %d > %d", radius, sm::kMaxFastRadius);
+    const DsliceCfg cfg{width, height, radius, num_disp, guided, (flags & SM_LR_CHECK) != 0};
+    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius)
+        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d (the fused right view)", radius,
+                    sm::kMaxBoxRadius);
     if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
         return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
     const int64_t P = (int64_t)width * height;
     const int n = members;
     const DslicePlan p0 = dslice_plan(P, num_disp, n, 0, height);
     // workspace: one member's layout (its gathered frames are the all-gather's result, shared by every
-    // rehearsed member) followed by the other members' key maps [n - 1][padded]
-    const DsliceWs w = dslice_ws(nullptr, p0, n, width);
-    rc = ensure_dsl(h, w.bytes + (size_t)((n - 1) * p0.padded * 4));
+    // rehearsed member) followed by the other members' key maps [n - 1][padded] (and right key maps)
+    const DsliceWs w = dslice_ws(nullptr, p0, n, width, cfg.lr);
+    const int nk = cfg.lr ? 2 : 1;
+    rc = ensure_dsl(h, w.bytes + (size_t)(nk * (n - 1) * p0.padded * 4));
     if (rc) return rc;
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = h->stream;
-    const DsliceWs ws = dslice_ws(h->d_dsl, p0, n, width);
+    const DsliceWs ws = dslice_ws(h->d_dsl, p0, n, width, cfg.lr);
     uint32_t* extra = reinterpret_cast<uint32_t*>(h->d_dsl + w.bytes);
     auto keys_of = [&](int k) { return k == 0 ? ws.keys : extra + (int64_t)(k - 1) * p0.padded; };
+    auto rkeys_of = [&](int k) {
+        return !cfg.lr ? nullptr : k == 0 ? ws.rkeys : extra + (int64_t)(n - 1 + k - 1) * p0.padded;
+    };
     uint8_t* map = ws.map;
     // the row-split upload: member k's rows into slot k of the gathered frames, which is where the
     // in-place all-gather leaves them on every member; the pad rows of the last slots are never read
@@ -1795,21 +1923,33 @@ SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_
         rc = dslice_upload_rows(dslice_plan(P, num_disp, n, k, height), ws, k, left, right, width, pitch, s);
         if (rc) return rc;
     }
-    for (int k = 0; k < n; ++k) {   // every member's key pass, into its own buffer
-        rc = dslice_keys(h, dslice_plan(P, num_disp, n, k, height), ws.gl, ws.gr, width, height, radius, guided,
-                         keys_of(k), s);
+    for (int k = 0; k < n; ++k) {   // every member's key pass, into its own buffers
+        rc = dslice_keys(h, dslice_plan(P, num_disp, n, k, height), cfg, ws.gl, ws.gr, keys_of(k), rkeys_of(k), s);
         if (rc) return rc;
     }
-    // the reduce-scatter's MIN (into member 0's buffer), then each member's chunk finalised into
-    // the all-gather's slot k
-    for (int k = 1; k < n; ++k)
-        SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.keys), reinterpret_cast<const int*>(keys_of(k)),
-                                   p0.padded, s));
+    // the reduce-scatter's MIN (into member 0's buffers: signed for guided keys, unsigned for box keys,
+    // whose right-view keys carry no seed), then each member's chunk finalised into the all-gather's slot k
+    for (int k = 1; k < n; ++k) {
+        if (guided) {
+            SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.keys), reinterpret_cast<const int*>(keys_of(k)),
+                                       p0.padded, s));
+            if (cfg.lr)
+                SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.rkeys), reinterpret_cast<const int*>(rkeys_of(k)),
+                                           p0.padded, s));
+        } else {
+            SM_HIP(sm::launch_min_keys_u32(ws.keys, keys_of(k), p0.padded, s));
+            if (cfg.lr) SM_HIP(sm::launch_min_keys_u32(ws.rkeys, rkeys_of(k), p0.padded, s));
+        }
+    }
     for (int k = 0; k < n; ++k) {
         const DslicePlan p = dslice_plan(P, num_disp, n, k, height);
         rc = dslice_finalise(ws.keys + k * p.chunk, p.chunk, radius, guided, map + k * p.chunk, s);
         if (rc) return rc;
+        if (cfg.lr) SM_HIP(sm::launch_keys_low_byte(ws.rkeys + k * p.chunk, p.chunk, ws.rmap + k * p.chunk, s));
     }
+    if (cfg.lr)
+        SM_HIP(sm::launch_lr_check(map, width, P, ws.rmap, width, P, 0, width, height, 1, map, width, P, nullptr, nullptr,
+                                   width, P, s));
     SM_HIP(copy2d(disp_out, out_pitch, map, width, width, height, hipMemcpyDeviceToHost, s));
     SM_HIP(hipStreamSynchronize(s));
     return SM_OK;

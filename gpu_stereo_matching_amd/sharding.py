@@ -134,20 +134,45 @@ def gather_disparity(chunk_u8, out_flat, group=None):
 
 
 GUIDED_EMPTY_KEY = 0x7FFFFFFF   # guided slice key of a pixel with no valid d (INT32_MAX)
+RIGHT_EMPTY_KEY = 0x7FFFFFFF    # right-view slice key of a pixel no d of the slice reaches (box and guided)
+
+
+def lr_check_host(left_disp, right_disp):
+    """numpy twin of sm_lr_check_device (StereoDisparity.cpp:136-147): d = dL(x); occluded when x - d < 0,
+    d == 0 or |d - dR(x - d)| > 1; returns (checked map, valid mask)."""
+    import numpy as np
+    dl = np.asarray(left_disp, np.int64)
+    dr = np.asarray(right_disp, np.int64)
+    H, W = dl.shape
+    x = np.arange(W)[None, :]
+    src = x - dl
+    inb = src >= 0
+    got = np.take_along_axis(dr, np.clip(src, 0, W - 1), axis=1)
+    occ = ~inb | (dl == 0) | (np.abs(dl - got) > 1)
+    return np.where(occ, 0, dl).astype(np.uint8), (~occ).astype(np.uint8)
 
 
 def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int, world: int,
-                 keys_t=None, out_t=None, stream=None, group=None, collective: str = "rs_ag", agg: str = "box"):
+                 keys_t=None, out_t=None, stream=None, group=None, collective: str = "rs_ag", agg: str = "box",
+                 lr_check: bool = False, right_bufs=None):
     """One frame, d-sharded over the process group: slice keys -> MIN reduce -> disparity.
 
     collective "rs_ag" (default): reduce-scatter the keys, convert this rank's chunk, all-gather
     uint8; "allreduce": MIN all-reduce of the whole key map, then convert.  keys_t / out_t: the
     flat buffers of dslice_buffers() (allocated when None).  agg "guided": the keys are the guided
     path's signed (q * 2^14) << 8 | d (the same MIN collectives; padding / empty slices hold
-    INT32_MAX, the threshold q < 50 is applied after the reduction).  Returns the [H, W] disparity."""
+    INT32_MAX, the threshold q < 50 is applied after the reduction).  lr_check: the slice pass also
+    emits the right view's keys (C_R(u, d) = C_L(u + d, d), StereoHelper.cpp:156-180, one fused pass:
+    sm_slice_keys_lr_device), which take the same MIN collective ("LR adds a second packed reduction
+    for the right view"); their d fields form dR and StereoDisparity.cpp:136-147 checks the
+    map.  right_bufs: a second dslice_buffers() pair for the right view (allocated when None).
+    Returns the [H, W] disparity."""
     import torch
     if collective not in ("rs_ag", "allreduce"):
         raise ValueError("collective must be 'rs_ag' or 'allreduce'")
+    if lr_check:
+        return _match_dslice_lr(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream,
+                                group, collective, agg, right_bufs)
     if agg == "box":
         fill = seed_key(radius)
         slice_keys = lambda lo, hi, k: matcher.slice_keys_device(left_t, right_t, radius, lo, hi,  # noqa: E731
@@ -188,6 +213,52 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
     return out_t[:P].view(H, W)
 
 
+def _match_dslice_lr(matcher, left_t, right_t, radius, num_disp, rank, world, keys_t, out_t, stream, group,
+                     collective, agg, right_bufs):
+    import torch
+    if agg not in ("box", "guided"):
+        raise ValueError("agg must be 'box' or 'guided'")
+    fill = GUIDED_EMPTY_KEY if agg == "guided" else seed_key(radius)
+    to_disp = ((lambda k, o=None: matcher.guided_keys_to_disp_device(k, out_t=o)) if agg == "guided"  # noqa: E731
+               else (lambda k, o=None: matcher.keys_to_disp_device(k, radius, out_t=o)))
+    lo, hi = dslice_bounds(num_disp, rank, world)
+    H, W = left_t.shape[-2:]
+    P = H * W
+    if keys_t is None or out_t is None:
+        keys_t, out_t = dslice_buffers(H, W, world, left_t.device)
+    rkeys_t, rout_t = right_bufs if right_bufs is not None else dslice_buffers(H, W, world, left_t.device)
+    n_pad = padded_pixels(H, W, world)
+    for t in (keys_t, out_t, rkeys_t, rout_t):
+        if t.numel() != n_pad:
+            raise ValueError("keys_t / out_t / right_bufs must be dslice_buffers(H, W, world)")
+    keys_img, rkeys_img = keys_t[:P].view(H, W), rkeys_t[:P].view(H, W)
+    if stream is not None:
+        stream.wait_stream(torch.cuda.current_stream(left_t.device))
+    if hi > lo:
+        matcher.slice_keys_lr_device(left_t, right_t, radius, lo, hi, agg=agg, keys_t=keys_img,
+                                     right_keys_t=rkeys_img, stream=stream)
+    else:
+        keys_img.fill_(fill)
+        rkeys_img.fill_(RIGHT_EMPTY_KEY)
+    keys_t[P:].fill_(fill)
+    rkeys_t[P:].fill_(RIGHT_EMPTY_KEY)
+    if stream is not None:
+        torch.cuda.current_stream(left_t.device).wait_stream(stream)
+    if collective == "allreduce":
+        reduce_slice_keys(keys_t, group)
+        reduce_slice_keys(rkeys_t, group)
+        to_disp(keys_t.view(1, -1), out_t.view(1, -1))
+        matcher.right_keys_to_disp_device(rkeys_t, out_t=rout_t)
+    else:
+        chunk = reduce_scatter_keys(keys_t, world, group)
+        rchunk = reduce_scatter_keys(rkeys_t, world, group)
+        n = chunk.numel()
+        gather_disparity(to_disp(chunk.view(1, n)).view(n), out_t, group)
+        gather_disparity(matcher.right_keys_to_disp_device(rchunk), rout_t, group)
+    img = out_t[:P].view(H, W)
+    return matcher.lr_check_device(img, rout_t[:P].view(H, W), out_t=img)
+
+
 GUIDED_SEED_Q = 50 * 16384   # q < 50 in the guided keys' 2^-14 fixed point (Device.cu:37 seed)
 
 
@@ -198,14 +269,30 @@ def guided_keys_to_disparity_host(keys):
     return np.where((k >> 8) < GUIDED_SEED_Q, k & 0xFF, 0).astype(np.uint8)
 
 
-def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_ag", group=None, agg: str = "box"):
+def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_ag", group=None, agg: str = "box",
+                           right_keys=None):
     """CPU (gloo) form of match_dslice's reduction for tests: this rank's [H, W] slice keys (int32
     numpy) -> the [H, W] uint8 disparity of the global minimum, through the same collectives.
-    agg "guided": signed guided keys, INT32_MAX padding, threshold q < 50."""
+    agg "guided": signed guided keys, INT32_MAX padding, threshold q < 50.  right_keys: this rank's
+    right-view slice keys; they take the same reduction, their d fields form dR, and the map is
+    LR-checked (lr_check_host) — match_dslice(lr_check=True)'s data flow."""
     import numpy as np
     import torch
     H, W = keys.shape
     P = H * W
+    if right_keys is not None:
+        left = match_dslice_host_keys(keys, radius, world, collective, group, agg)
+        flat = torch.full((padded_pixels(H, W, world),), RIGHT_EMPTY_KEY, dtype=torch.int32)
+        flat[:P] = torch.from_numpy(np.ascontiguousarray(right_keys, np.int32).reshape(P))
+        if collective == "allreduce":
+            reduce_slice_keys(flat, group)
+            right = (flat.numpy()[:P] & 0xFF).astype(np.uint8)
+        else:
+            chunk = reduce_scatter_keys(flat, world, group)
+            out = torch.empty(flat.numel(), dtype=torch.uint8)
+            gather_disparity(torch.from_numpy((chunk.numpy() & 0xFF).astype(np.uint8)), out, group)
+            right = out.numpy()[:P]
+        return lr_check_host(left, right.reshape(H, W))[0]
     if agg == "guided":
         fill = GUIDED_EMPTY_KEY
         finish = lambda k: guided_keys_to_disparity_host(k)   # noqa: E731

@@ -171,6 +171,27 @@ SM_API int sm_guided_slice_keys_device(sm_handle *h, const uint8_t *d_left, cons
 SM_API int sm_guided_keys_to_disp_device(sm_handle *h, const int32_t *d_keys, int width, int height,
                                          uint8_t *d_disp, int out_pitch, void *stream);
 
+/* d-slice keys of BOTH views from one fused pass (multi-GPU d-slices with the LR check, SURVEY §8e "LR adds
+ * a second packed reduction for the right view"): d_left_keys as sm_slice_keys_device (flags SM_AGG_BOX,
+ * uint32) or sm_guided_slice_keys_device (SM_AGG_GUIDED, int32), and d_right_keys the right view's keys,
+ * C_R(y, u, d) = C_L(y, u + d, d) (StereoHelper.cpp:156-180): per right pixel the minimum over d in
+ * [d_lo, d_hi) with u + d < W of (cost << 8) | d, no threshold (:131-154); box: (SAD << 8 | d), guided:
+ * (floor(q * 2^14) << 8 | d); INT32_MAX where no d of the slice reaches u.  Box keys (left and right) are
+ * below 2^31 at these radii, so right keys of disjoint slices combine with the same elementwise MIN as the
+ * left keys, signed or unsigned (guided: signed).  radius <= 15 (box) / <= 7 (guided).  Uses the handle's
+ * right-view workspace. */
+SM_API int sm_slice_keys_lr_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
+                                   int pitch, int radius, int d_lo, int d_hi, unsigned flags, void *d_left_keys,
+                                   void *d_right_keys, void *stream);
+
+/* Combined right-view keys -> dR: the d field (low byte) of each of n keys (box or guided). */
+SM_API int sm_right_keys_to_disp_device(sm_handle *h, const void *d_keys, int64_t n, uint8_t *d_disp, void *stream);
+
+/* The left-right check of StereoDisparity.cpp:136-147 on device maps: d = dL(x); occluded when x - d < 0, d == 0
+ * or |d - dR(x - d)| > 1; d_out = occluded ? 0 : d (may alias d_left_disp), d_mask (may be NULL) = !occluded. */
+SM_API int sm_lr_check_device(sm_handle *h, const uint8_t *d_left_disp, const uint8_t *d_right_disp, int width,
+                              int height, int pitch, uint8_t *d_out, uint8_t *d_mask, int out_pitch, void *stream);
+
 /* Wait for all work queued on `stream`.  NULL means the default stream, as it does for every
  * device entry point, and also waits for the handle's own stream. */
 SM_API int sm_stream_sync(sm_handle *h, void *stream);
@@ -322,7 +343,10 @@ SM_API int sm_group_block_match_batch_u8(sm_group *g, const uint8_t *const *left
  * uint8 (the Device.cu:37 threshold) and one RCCL all-gather assembles the map on every member;
  * member 0's copy is downloaded into disp_out.  Bit-identical to sm_block_match_u8 for box
  * aggregation; guided keys quantise q to 2^-14, so two fp32 costs closer than that may resolve
- * differently from a single pass.  flags: 0 (box) or SM_AGG_GUIDED.  Members must be distinct
+ * differently from a single pass.  flags: 0 (box) or SM_AGG_GUIDED, optionally | SM_LR_CHECK: each
+ * member also emits the right view's keys for its slice from the same fused pass
+ * (sm_slice_keys_lr_device), a second MIN reduce-scatter + all-gather forms dR, and member 0 applies
+ * StereoDisparity.cpp:136-147 before the download (box LR: radius <= 15).  Members must be distinct
  * devices; RCCL (librccl.so.1) is loaded on first use and one communicator per member is created
  * with ncclCommInitAll.
  * Failure handling: the call runs in two phases.  Phase 1 (upload, slice keys, stream sync) runs on
@@ -350,7 +374,8 @@ SM_API int sm_dslice_plan(int64_t pixels, int num_disp, int members, int member,
  * finalisation; the RCCL MIN reduce-scatter is an elementwise MIN of their key maps and the
  * all-gather puts chunk k at offset k*chunk.  The map must equal sm_block_match_u8's (box) for any
  * member count; it lets the plan for n > 1 be checked on a one-GPU machine.  flags: 0 or
- * SM_AGG_GUIDED; members 1..64.  Synchronous. */
+ * SM_AGG_GUIDED, optionally | SM_LR_CHECK (the right keys' MIN and the LR check as in the group call);
+ * members 1..64.  Synchronous. */
 SM_API int sm_dslice_rehearse_u8(sm_handle *h, const uint8_t *left, const uint8_t *right, int width,
                                  int height, int pitch, int radius, int num_disp, unsigned flags,
                                  int members, uint8_t *disp_out, int out_pitch);

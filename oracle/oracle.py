@@ -221,6 +221,23 @@ def box_keys_slice(left, right, radius: int, d_lo: int, d_hi: int) -> np.ndarray
     return keys
 
 
+def box_right_keys_slice(left, right, radius: int, d_lo: int, d_hi: int, cost: np.ndarray = None) -> np.ndarray:
+    """Right-view d-slice keys (the contract of sm_slice_keys_lr_device's right map, box): for right pixel u
+    the minimum over d in [d_lo, d_hi) with u + d < W of (C_L(u + d, d) << 8 | d), C_R(u, d) = C_L(u + d, d)
+    (StereoHelper.cpp:156-180), 0x7FFFFFFF where no d of the slice reaches u.  uint32 [H, W].  `cost`: a
+    box_cost volume of at least d_hi planes (computed when None)."""
+    if cost is None:
+        cost = box_cost(left, right, radius, d_hi)
+    _, H, W = cost.shape
+    best = np.full((H, W), 0x7FFFFFFF, np.int64)
+    for d in range(d_lo, d_hi):
+        if d >= W:
+            break
+        k = (cost[d][:, d:].astype(np.int64) << 8) | d
+        best[:, :W - d] = np.minimum(best[:, :W - d], k)
+    return best.astype(np.uint32)
+
+
 def right_wta(cost: np.ndarray) -> np.ndarray:
     cost = np.ascontiguousarray(cost, dtype=np.int32)
     D, H, W = cost.shape

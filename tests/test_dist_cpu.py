@@ -61,6 +61,55 @@ def test_dslice_min_reduction_gloo(tmp_path, world, D, W):
         assert (np.load(tmp_path / f"frames{k}.npy") == 1).all()
 
 
+def _lr_worker(rank, world, port, W, H, r, D, result_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    L, R = O.synth_pair(77, W, H, max(D, 16))
+    lo, hi = sharding.dslice_bounds(D, rank, world)
+    if hi > lo:
+        keys = O.box_keys_slice(L, R, r, lo, hi).view(np.int32)
+        rkeys = O.box_right_keys_slice(L, R, r, lo, hi).view(np.int32)
+    else:
+        keys = np.full((H, W), sharding.seed_key(r), np.int32)
+        rkeys = np.full((H, W), sharding.RIGHT_EMPTY_KEY, np.int32)
+    for coll in ("allreduce", "rs_ag"):
+        disp = sharding.match_dslice_host_keys(keys, r, world, collective=coll, right_keys=rkeys)
+        np.save(os.path.join(result_dir, f"lr{rank}_{coll}.npy"), disp)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,D,W", [(2, 48, 90), (3, 37, 61), (4, 3, 50)])
+def test_dslice_lr_reduction_gloo(tmp_path, world, D, W):
+    """d-slices with the LR check (a second packed reduction for the right view): the right
+    view's slice keys take the same MIN collectives, their d fields form dR, and StereoDisparity.cpp:136-147
+    gives the single pass's checked map (box_lr) on every rank, through both collectives, with empty slices
+    (world 4 > D 3) and padded pixel counts."""
+    H, r = 30, 3
+    port = _free_port()
+    mp.spawn(_lr_worker, args=(world, port, W, H, r, D, str(tmp_path)), nprocs=world, join=True)
+    from oracle import oracle as O
+    L, R = O.synth_pair(77, W, H, max(D, 16))
+    want = O.box_lr(L, R, r, D)[2]
+    assert want.any()
+    for k in range(world):
+        for coll in ("allreduce", "rs_ag"):
+            assert np.array_equal(np.load(tmp_path / f"lr{k}_{coll}.npy"), want), (k, coll)
+
+
+def test_right_keys_slice_min_is_right_wta():
+    """The right view's slice keys MIN'ed over any partition of [0, D) give STMatching's right WTA
+    (StereoHelper.cpp:131-180: the clamped walk, strict < from d = 0) on the oracle's cost volume."""
+    from oracle import oracle as O
+    L, R = O.synth_pair(5, 70, 20, 32)
+    cost = O.box_cost(L, R, 2, 32)
+    want = O.right_wta(cost)
+    for cuts in ((0, 32), (0, 5, 32), (0, 1, 2, 17, 31, 32)):
+        k = np.minimum.reduce([O.box_right_keys_slice(L, R, 2, a, b, cost) for a, b in zip(cuts, cuts[1:])])
+        assert np.array_equal((k & 0xFF).astype(np.uint8), want), cuts
+
+
 def _guided_slice_keys(q, lo, hi):
     """Host restatement of sm_guided_slice_keys_device on the oracle's fp64 q volume [D][H][W]:
     (int)(q * 2^14) << 8 | d over the valid d (d <= W - x) of [lo, hi), INT32_MAX if none."""
