@@ -537,6 +537,36 @@ def main():
                               f"x{world}", "value": round(B5 * world * n5 / dt5, 2), "unit": "disparity-maps/s",
                     "ms_per_step": round(dt5 * 1000 / n5, 4), "steps": n5, "n_gpus": world, "scaling": "weak",
                     "kernel": "guided_fused_kernel<5, true>", "dtype": "fp32 (u8 in/out)"}
+            if distributed:
+                # the north star's split on the configuration it pays for: ONE 4K guided + LR
+                # frame d-sharded over the ranks, left and right keys through two MIN reduce-scatters, the
+                # LR check on the gathered maps (sharding.match_dslice(lr_check=True))
+                from gpu_stereo_matching_amd import sharding
+                m5.set_guided_eps(1e-4 * 255 * 255)
+                kb5 = sharding.dslice_buffers(H5, W5, world, dev)
+                rb5 = sharding.dslice_buffers(H5, W5, world, dev)
+
+                def dstep5():
+                    sharding.match_dslice(m5, L5[0], R5[0], r, D5, rank, world, keys_t=kb5[0], out_t=kb5[1],
+                                          stream=stream, agg="guided", lr_check=True, right_bufs=rb5)
+
+                for _ in range(2):
+                    dstep5()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                t1 = time.perf_counter()
+                for _ in range(n5):
+                    dstep5()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                cfg5["dslice_guided_lr"] = {
+                    "config": f"cfg5 one {W5}x{H5} frame, guided + LR, d_max={D5}, d-sharded over {world} ranks: "
+                              f"left + right slice keys, two MIN reduce_scatter int32 + two all_gather uint8 "
+                              f"({backend}), LR check", "value": round(n5 / float(t.item()), 2),
+                    "unit": "disparity-maps/s", "ms_per_frame": round(float(t.item()) * 1000 / n5, 4),
+                    "scaling": "strong", "keys_bytes_per_frame": W5 * H5 * 8}
         finally:
             m5.close()
 

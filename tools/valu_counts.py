@@ -52,7 +52,7 @@ def main():
             for row in csv.DictReader(open(f)):
                 if kname in row["Kernel_Name"]:
                     vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-        if "guided" in name or "box_lr" in name:
+        if "guided" in name or "box_lr" in name or name.startswith("box_r5"):   # + the headline
             d2 = d + "_wait"
             cmd2 = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc"] + WAIT_CTRS.split() + [
                 "-d", d2, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
