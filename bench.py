@@ -98,6 +98,31 @@ def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None):
            "lds_busy_frac": round(pl["SQ_LDS_IDX_ACTIVE"] / (256 * t * CU_CLOCK_HZ), 4)
            if "SQ_LDS_IDX_ACTIVE" in pl else None,
            "counts_source": "profiles/valu_counts.json (rocprofv3 --pmc SQ_INSTS_VALU, tools/valu_counts.py)"}
+    # issue-cycle-weighted VALU busy: each wave64 VALU instruction costs the SIMD the cycles
+    # measured for its encoding on this part (profiles/microbench/r02_valu_issue_cycles_pmc.txt: 2.37 for 32-bit
+    # VOP1/VOP2, 4.25 for VOP3 such as v_perm_b32 / v_sad_u8 / v_min3_u32, 3.9 for conversions), averaged over
+    # the kernel's unmasked main-loop iteration in the gfx950 ISA (profiles/isa_mix_box.json, tools/isa_mix.py);
+    # SQ_INSTS_VALU x that average / (1024 SIMDs x launch cycles) is the share of the SIMDs' VALU issue
+    # capacity the kernel uses with its own instruction mix
+    try:
+        with open(os.path.join(ROOT, "profiles", "isa_mix_box.json")) as f:
+            mix = json.load(f)
+    except (OSError, ValueError):
+        mix = None
+    if mix and key.startswith("box_r5"):
+        cyc = pl["SQ_INSTS_VALU"] * mix["avg_cycles_per_valu"]
+        res["valu_issue_busy"] = round(cyc / (1024 * t * CU_CLOCK_HZ), 4)
+        res["valu_avg_cycles_per_inst"] = mix["avg_cycles_per_valu"]
+        res["valu_issue_note"] = ("SQ_INSTS_VALU x measured issue cycles per instruction of the main-loop mix "
+                                  f"({mix['valu_per_iteration']} VALU, {mix['issue_cycles_per_iteration']} cycles "
+                                  "per wave and disparity pair) / SIMD cycles: the fraction of VALU issue capacity "
+                                  "busy at this mix")
+    W_, H_, D_, _r, B_ = workload
+    res["lane_ops_per_pixel_d"] = round(pl["SQ_INSTS_VALU"] * 64 / (W_ * H_ * D_ * B_), 3)
+    if "SQ_WAVE_CYCLES" in pl:
+        res["wave_cycle_shares"] = {"issuing": round(pl["share_active_inst_any"], 4),
+                                    "waiting_waitcnt_barrier": round(pl["share_wait_any"], 4),
+                                    "issue_stalled": round(pl["share_wait_inst_any"], 4)}
     if extra:
         res.update(extra)
     return res

@@ -272,7 +272,16 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     const int d_free = a.valid_mode == 0 ? W - xmax_tile : x0;
     const bool r_out = RIGHT && x0 + G::TW > W;
     const bool col_in = (c >= 0) && (c < W);
-    const int npairs = dspan >> 1;                 // multiple of 4
+    int npairs = dspan >> 1;                       // multiple of 4
+    if constexpr (!RIGHT) {
+        // pairs whose d exceeds the largest d valid for ANY output of the tile (W - x0 for the left view,
+        // Device.cu:44's break; x_max mirrored) leave every key of the tile unchanged: the tile's waves split
+        // only the pairs below (round 5: the right-edge tiles skip their all-invalid pairs instead of running
+        // them through the masked phase H; the right view (RIGHT) still needs their raw keys)
+        const int dv = a.valid_mode == 0 ? W - x0 : xmax_tile;
+        const int pe = dv < d_lo ? 0 : ((dv - d_lo) >> 1) + 1;
+        npairs = pe < npairs ? pe : npairs;
+    }
     const int p_lo = (wave * npairs) / NW;
     const int p_hi = ((wave + 1) * npairs) / NW;
     uint32_t* csw = cs + wave * (G::HALF * G::CSS);   // this wave's private half-tile CS plane

@@ -675,23 +675,26 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         __syncthreads();
     };
     if (is_s1v) s1v(0, std::true_type{}, std::false_type{});
-    const bool s1_nomask = px0 >= D - 1 && px0 >= 0 && px0 + 63 < W;
-    const bool s2_lim = valid_mode != 1 ? (D - 1 > W - (x0 + G::TW - 1)) : (D - 1 > x0);
+    // (round 5: stopping the left-only kernel at the tile's last valid d, W - x0, measured +0.7 % slower on the
+    // 1080p guided launch (453.5 -> 456.9 us per frame, profiles/microbench/r05_skip_invalid_pairs_ab.txt): not kept)
+    const int Dk = D;
+    const bool s1_nomask = px0 >= Dk - 1 && px0 >= 0 && px0 + 63 < W;
+    const bool s2_lim = valid_mode != 1 ? (Dk - 1 > W - (x0 + G::TW - 1)) : (Dk - 1 > x0);
     lds_barrier();
     s1h_stats();
     __syncthreads();
     // buffers: cs (S1V -> S1H), abp (S1H -> S2V), mm (S2V -> S2H); each producer of iteration d+1
     // runs after the barrier that ends the consumer of iteration d.  The right band (read only by
     // S1V) is restaged for the next d-chunk in the second phase of the chunk's last iteration.
-    for (int d = d_lo; d <= D; ++d) {
-        if (is_s1v && d < D) {
+    for (int d = d_lo; d <= Dk; ++d) {
+        if (is_s1v && d < Dk) {
             if (s1_nomask) s1v(d, std::false_type{}, std::true_type{});
             else s1v(d, std::false_type{}, std::false_type{});
         }
         if ((!ROLES || !is_s1v) && d > d_lo) s2v();
         lds_barrier();
-        if (d + 1 < D && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
-        if (d < D) s1h();
+        if (d + 1 < Dk && ((d + 1) & (kBandChunk - 1)) == 0) stage_band((d + 1) / kBandChunk);
+        if (d < Dk) s1h();
         if (d > d_lo) {
             if (s2_lim) s2h(d - 1, std::true_type{});
             else s2h(d - 1, std::false_type{});

@@ -5,6 +5,7 @@ from the measured per-instruction rates on this part (profiles/microbench/r02_va
 encodings ~4.25, conversions 3.9, v_cndmask 3.24).
 
     python tools/isa_mix.py build/bm_box.s 'box_match_kernelILi5ELi128ELb0ELi4E'
+    python tools/isa_mix.py --json build/bm_box.s 'box_match_kernelILi5ELi128ELb0ELi4E' > profiles/isa_mix_box.json
 """
 import collections
 import re
@@ -52,7 +53,52 @@ def kernel_lines(path, name):
     return out
 
 
+def loop_blocks(lines, a, b):
+    """basic blocks of lines[a..b]: (label, VALU count, issue cycles, opcode Counter)"""
+    blocks, cur = [], None
+    for ln in lines[a:b + 1]:
+        m = re.match(r"^(\.LBB\S+):", ln)
+        if m:
+            cur = [m.group(1), 0, 0.0, collections.Counter()]
+            blocks.append(cur)
+            continue
+        m = re.match(r"^\s+(v_\w+)\s*(.*)", ln)
+        if m and cur is not None:
+            cur[1] += 1
+            cur[2] += weight(m.group(1), m.group(2))
+            cur[3][m.group(1)] += 1
+    return blocks
+
+
+def hot_path(path, name, exclude_op="v_cmp_lt_i32_e64"):
+    """The largest loop's blocks without `exclude_op` (for box_match_kernel: the unmasked pair iteration,
+    the masked phase-H blocks compare every output's d against its validity limit): VALU per iteration,
+    issue cycles, average cycles per VALU instruction and the opcode mix."""
+    lines = kernel_lines(path, name)
+    labels = {m.group(1): i for i, ln in enumerate(lines) for m in [re.match(r"^(\.LBB\S+):", ln)] if m}
+    loops = []
+    for i, ln in enumerate(lines):
+        m = re.match(r"^\s+s_(cbranch_\w+|branch)\s+(\.LBB\S+)", ln)
+        if m and m.group(2) in labels and labels[m.group(2)] < i:
+            loops.append((labels[m.group(2)], i))
+    a, b = max(loops, key=lambda t: t[1] - t[0])
+    n, cyc, mix = 0, 0.0, collections.Counter()
+    for lab, cnt, c, ops in loop_blocks(lines, a, b):
+        if exclude_op in ops:
+            continue
+        n += cnt
+        cyc += c
+        mix += ops
+    return {"kernel": name, "valu_per_iteration": n, "issue_cycles_per_iteration": round(cyc, 1),
+            "avg_cycles_per_valu": round(cyc / n, 4), "mix": dict(mix.most_common()),
+            "excluded_blocks_with": exclude_op}
+
+
 def main():
+    if sys.argv[1] == "--json":
+        import json
+        print(json.dumps(hot_path(sys.argv[2], sys.argv[3]), indent=1))
+        return
     path, name = sys.argv[1], sys.argv[2]
     lines = kernel_lines(path, name)
     labels = {}
