@@ -243,6 +243,9 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     const int64_t PB = P * batch;
     const bool fused_right = lr && !guided && radius <= sm::kMaxBoxRadius;
     const bool guided_right = lr && guided;   // right view fused into the guided pass (bm_guided.hip)
+    // box r > 15: the separable wide-window path (bm_wide.hip), right view included; wider frames keep the
+    // direct generic kernel and the mirrored LR pass
+    const bool wide = !guided && radius > sm::kMaxBoxRadius && W <= sm::kMaxWideWidth;
     if ((flags & SM_DEVICE_CU_GRID) != 0) {   // Device.cu's launch geometry, frame by frame (bm_literal.hip)
         if (flags != SM_DEVICE_CU_GRID || lr)
             return fail(SM_ERR_INVALID_ARG, "SM_DEVICE_CU_GRID is box aggregation only (flags 0x%x)", flags);
@@ -266,7 +269,7 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     }
 
     // workspace: [left raw (med)] [right (lr)] [right filtered (lr && med)] [mirrored L, R (lr, not fused)]
-    const bool mirrored = lr && !fused_right && !guided_right;
+    const bool mirrored = lr && !fused_right && !guided_right && !wide;
     const int64_t n_planes = (med ? 1 : 0) + (lr ? 1 : 0) + (lr && med ? 1 : 0) + (mirrored ? 2 : 0);
     if (n_planes > 0) {
         int rc = ensure_lr(h, (size_t)(n_planes * PB));
@@ -321,6 +324,11 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     } else if (guided) {
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
+    } else if (wide) {
+        int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D));
+        if (rc) return rc;
+        SM_HIP(sm::launch_box_match_wide(a, batch, reinterpret_cast<uint16_t*>(h->d_vol), lr ? right_map : nullptr, W,
+                                         P, s));
     } else {
         SM_HIP(sm::launch_box_match(a, batch, s));
     }
@@ -764,6 +772,12 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
     a.thresh_key = seed_key(radius);
     a.keys = keys;
     if (!rkeys) {
+        if (radius > sm::kMaxBoxRadius && W <= sm::kMaxWideWidth) {   // the wide-window path (bm_wide.hip)
+            int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo));
+            if (rc) return rc;
+            SM_HIP(sm::launch_box_match_wide(a, 1, reinterpret_cast<uint16_t*>(h->d_vol), nullptr, 0, 0, s));
+            return SM_OK;
+        }
         SM_HIP(sm::launch_box_match(a, 1, s));
         return SM_OK;
     }
@@ -1187,23 +1201,17 @@ SM_API int sm_slice_keys_device(sm_handle* h, const uint8_t* d_left, const uint8
     if (!d_left || !d_right || !d_keys) return fail(SM_ERR_INVALID_ARG, "null device pointer");
     SM_HIP(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    sm::MatchArgs a{};
-    a.left = d_left;
-    a.right = d_right;
-    a.W = width;
-    a.H = height;
-    a.pitch = pitch;
-    a.frame_stride = (int64_t)pitch * height;
-    a.radius = radius;
-    a.d_lo = d_lo;
-    a.d_hi = d_hi;
-    a.valid_mode = 0;
-    a.seed_key = seed_key(radius);
-    a.thresh_key = seed_key(radius);
-    a.disp = nullptr;
-    a.keys = d_keys;
-    SM_HIP(sm::launch_box_match(a, 1, s));
-    return SM_OK;
+    // radius > 15 runs the wide-window path through the handle's volume workspace: ordered after the handle's
+    // last workspace pass on another stream, as run_device orders its passes
+    const bool ws = radius > sm::kMaxBoxRadius && width <= sm::kMaxWideWidth;
+    if (ws && h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
+    rc = slice_keys_pass(h, d_left, d_right, width, height, pitch, radius, d_lo, d_hi, false, d_keys, nullptr, s);
+    if (ws) {
+        SM_HIP(hipEventRecord(h->scratch_ev, s));
+        h->scratch_stream = s;
+        h->scratch_pending = true;
+    }
+    return rc;
 }
 
 SM_API int sm_keys_to_disp_device(sm_handle* h, const uint32_t* d_keys, int width, int height, int radius,

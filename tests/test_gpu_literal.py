@@ -150,3 +150,57 @@ def test_wide_radius_lr(matcher, oracle, r):
     chk, rd, mask = matcher.match_lr(L, R, r, D)
     _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, r, D)
     assert np.array_equal(rd, rd_o) and np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+
+
+# ---- the separable wide-window path (bm_wide.hip, radius 16..127, width <= 4096) ----
+
+@pytest.mark.parametrize("W,H,r,D", [(1920, 1080, 20, 128), (333, 77, 16, 256), (4096, 40, 40, 24), (61, 300, 99, 7)])
+def test_wide_path_bit_exact_sizes(matcher, oracle, W, H, r, D):
+    """Full HD at r = 20, D = 256, the 4096-column limit (16 outputs per thread), a narrow tall frame."""
+    if W > 2048:
+        import gpu_stereo_matching_amd as sm
+        m = sm.BlockMatcher(0, 4096, 64, 64)
+    else:
+        m = matcher
+    L, R = oracle.synth_pair(40 + r, W, H, max(D, 16))
+    assert np.array_equal(m.match(L, R, r, D), oracle.box_disp(L, R, r, D))
+
+
+def test_wide_path_fallback_past_4096_columns(oracle):
+    """Wider than 4096 columns: the direct generic kernel (correct, not fast)."""
+    import gpu_stereo_matching_amd as sm
+    L, R = oracle.synth_pair(9, 4100, 6, 16)
+    with sm.BlockMatcher(0, 4100, 8, 16) as m:
+        assert np.array_equal(m.match(L, R, 16, 4), oracle.box_disp(L, R, 16, 4))
+
+
+@pytest.mark.parametrize("r,D", [(16, 64), (31, 48), (127, 12)])
+def test_wide_path_lr_and_median_device_batch(sm, matcher, oracle, r, D):
+    """The right view from the same row pass (C_R(u, d) = C_L(u + d, d)), with and without the 7x7 median,
+    batched on the device: every frame equal to the oracle's LR maps."""
+    import torch
+    pairs = [oracle.synth_pair(70 + i, 180, 60, max(D, 16)) for i in range(3)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D, lr_check=True)
+    torch.cuda.synchronize()
+    for i, (L, R) in enumerate(pairs):
+        assert np.array_equal(out[i].cpu().numpy(), oracle.box_lr(L, R, r, D)[2]), i
+    chk, rd, mask = matcher.match_lr(pairs[0][0], pairs[0][1], r, D, median=True)
+    _, cost = oracle.box_disp(pairs[0][0], pairs[0][1], r, D, want_cost=True)
+    left_m = oracle.median(oracle.box_disp(pairs[0][0], pairs[0][1], r, D), 3)
+    right_m = oracle.median(oracle.right_wta(cost), 3)
+    chk_o, mask_o = oracle.lr_check(left_m, right_m)
+    assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
+
+
+def test_wide_path_slice_keys(matcher, oracle):
+    """d-slice keys at r > 15 (sm_slice_keys_device through the wide path) equal the oracle's keys."""
+    import torch
+    L, R = oracle.synth_pair(12, 300, 90, 64)
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    for a, b in ((0, 20), (20, 64), (63, 64)):
+        k = matcher.slice_keys_device(Lt, Rt, 21, a, b)
+        torch.cuda.synchronize()
+        assert np.array_equal(k.cpu().numpy().view(np.uint32), oracle.box_keys_slice(L, R, 21, a, b)), (a, b)
+    assert np.array_equal(matcher.dslice_rehearse(L, R, 21, 64, 3), oracle.box_disp(L, R, 21, 64))
