@@ -41,7 +41,26 @@ __global__ __launch_bounds__(kWT) void wide_vsum_kernel(const uint8_t* __restric
     uint32_t s = 0;
     const int y0e = min(radius, H - 1);
     for (int y = 0; y <= y0e; ++y) s += ad(y);
-    for (int y = 0; y < H; ++y) {
+    // rows in blocks of kU: the kU entering and kU leaving rows of a block are loaded before the running sum
+    // consumes them (the loads of one row are independent of s), so their latencies overlap
+    constexpr int kU = 8;
+    int y = 0;
+    for (; y + kU <= H; y += kU) {
+        uint32_t ain[kU], aout[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const int ya = y + k + radius + 1, yb = y + k - radius;
+            ain[k] = ya < H ? ad(ya) : 0u;
+            aout[k] = yb >= 0 ? ad(yb) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            Vd[(int64_t)(y + k) * W] = (uint16_t)s;
+            s += ain[k];
+            s -= aout[k];
+        }
+    }
+    for (; y < H; ++y) {
         Vd[(int64_t)y * W] = (uint16_t)s;
         const int ya = y + radius + 1, yb = y - radius;
         if (ya < H) s += ad(ya);
@@ -49,8 +68,10 @@ __global__ __launch_bounds__(kWT) void wide_vsum_kernel(const uint8_t* __restric
     }
 }
 
-// NPT outputs per thread (W <= 256 * NPT).  Dynamic LDS: pref[2][256 * NPT + 1] u32 (double-buffered over d,
-// so two barriers per d), then rmin[256 * NPT] u32 when the right view is requested.
+// NPT outputs per thread (W <= 256 * NPT), contiguous: x in [8t, 8t + 8) for NPT 8.  The prefix row lives in LDS
+// with one pad dword after every 8 (index i -> i + i / 8), so the 64 lanes' segment stores and their window
+// reads (lanes 9 dwords apart) fall on distinct banks.  Dynamic LDS: pref[2][NPAD] u32 (double-buffered over
+// d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.
 template <int NPT>
 __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restrict__ V, int W, int H, int radius,
                                                         int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
@@ -58,34 +79,53 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
                                                         uint32_t* __restrict__ keys, uint8_t* __restrict__ right,
                                                         int rpitch) {
     extern __shared__ __attribute__((aligned(16))) uint32_t wl[];
-    constexpr int NP = kWT * NPT + 1;
+    constexpr int NX = kWT * NPT + 1;                 // prefix entries 0..256 NPT
+    constexpr int NPAD = NX + NX / 8 + 1;
     __shared__ uint32_t wsum[2][kWT / 64];
-    uint32_t* rmin = wl + 2 * NP;
+    uint32_t* rmin = wl + 2 * NPAD;
+    auto pad = [](int i) { return i + (i >> 3); };
     const int y = blockIdx.x;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int x0 = t * NPT;
     const bool want_right = right != nullptr;
     if (want_right)
-        for (int i = t; i < kWT * NPT; i += kWT) rmin[i] = 0xFFFFFFFFu;
+        for (int i = t; i < NPAD; i += kWT) rmin[i] = 0xFFFFFFFFu;   // indexed pad(u), as pref
     uint32_t best[NPT];
     int lo[NPT], hi[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         best[k] = seed;
         const int x = x0 + k;
-        lo[k] = max(x - radius, 0);                  // window columns [lo, hi] (Device.cu:51)
-        hi[k] = min(x + radius, W - 1) + 1;
+        lo[k] = pad(max(x - radius, 0));              // window columns [lo, hi) of the prefix (Device.cu:51)
+        hi[k] = pad(min(x + radius, W - 1) + 1);
     }
+    const bool vec = (W % 8) == 0 && (NPT % 8) == 0;   // 16-B rows: 8 u16 per load
     for (int d = d_lo; d < d_hi; ++d) {
         const int b = (d - d_lo) & 1;
-        uint32_t* pref = wl + b * NP;
+        uint32_t* pref = wl + b * NPAD;
         const uint16_t* row = V + ((int64_t)(d - d_lo) * H + y) * W;
         uint32_t p[NPT];
         uint32_t acc = 0;
+        if (vec) {
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            acc += x0 + k < W ? (uint32_t)row[x0 + k] : 0u;
-            p[k] = acc;
+            for (int k = 0; k < NPT; k += 8) {
+                uint4 q = make_uint4(0, 0, 0, 0);
+                if (x0 + k < W) q = *reinterpret_cast<const uint4*>(row + x0 + k);
+                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc += w4[j] & 0xFFFFu;
+                    p[k + 2 * j] = acc;
+                    acc += w4[j] >> 16;
+                    p[k + 2 * j + 1] = acc;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                acc += x0 + k < W ? (uint32_t)row[x0 + k] : 0u;
+                p[k] = acc;
+            }
         }
         // inclusive scan of the per-thread totals across the wave, then the waves' offsets
         uint32_t inc = acc;
@@ -101,7 +141,7 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
         for (int w = 0; w < kWT / 64; ++w) base += w < wv ? wsum[b][w] : 0u;
         if (t == 0) pref[0] = 0u;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) pref[x0 + k + 1] = base + p[k];
+        for (int k = 0; k < NPT; ++k) pref[pad(x0 + k + 1)] = base + p[k];
         __syncthreads();
         const uint32_t dd = (uint32_t)(d & 0xFF);
 #pragma unroll
@@ -110,7 +150,7 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
             if (x < W) {
                 const uint32_t key = ((pref[hi[k]] - pref[lo[k]]) << 8) | dd;
                 if (d <= W - x) best[k] = min(best[k], key);       // Device.cu:44
-                if (want_right && x >= d) rmin[x - d] = min(rmin[x - d], key);
+                if (want_right && x >= d) rmin[pad(x - d)] = min(rmin[pad(x - d)], key);
             }
         }
     }
@@ -121,7 +161,7 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
         if (x < W) {
             if (disp) disp[(int64_t)y * opitch + x] = best[k] < thresh ? (uint8_t)(best[k] & 0xFFu) : (uint8_t)0;
             if (keys) keys[(int64_t)y * W + x] = best[k];
-            if (want_right) right[(int64_t)y * rpitch + x] = (uint8_t)(rmin[x] & 0xFFu);   // no threshold
+            if (want_right) right[(int64_t)y * rpitch + x] = (uint8_t)(rmin[pad(x)] & 0xFFu);   // no threshold
         }
     }
 }
@@ -129,7 +169,8 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
 template <int NPT>
 hipError_t launch_h(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
                     uint8_t* disp, int opitch, uint32_t* keys, uint8_t* right, int rpitch, hipStream_t s) {
-    const size_t lds = (size_t)(2 * (kWT * NPT + 1) + (right ? kWT * NPT : 0)) * 4;
+    constexpr int NX = kWT * NPT + 1;
+    const size_t lds = (size_t)((right ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
     hipLaunchKernelGGL(wide_hwta_kernel<NPT>, dim3((unsigned)H), dim3(kWT), lds, s, V, W, H, radius, d_lo, d_hi, seed,
                        thresh, disp, opitch, keys, right, rpitch);
     return hipGetLastError();
