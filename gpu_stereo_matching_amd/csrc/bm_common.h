@@ -90,6 +90,8 @@ size_t wide_workspace_bytes(int W, int H, int D);
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s);
 constexpr int kMaxWideWidth = 4096;
+// radius 16..127 and 4 <= W <= 4096 take the separable wide-window path (bm_wide.hip); the rest the generic kernel
+inline bool wide_path(int radius, int W) { return radius > kMaxBoxRadius && W >= 4 && W <= kMaxWideWidth; }
 // SM_DEVICE_CU_GRID (bm_literal.hip): Device.cu's literal map, AD only for rows < 256 and cols < 320, all zero
 // for W > 1024; needs W >= 320, H >= 256 and literal_workspace_bytes(D) of device scratch in `ws`
 size_t literal_workspace_bytes(int D);

@@ -21,51 +21,113 @@ namespace {
 
 constexpr int kWT = 256;
 
-__global__ __launch_bounds__(kWT) void wide_vsum_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
-                                                        int W, int H, int pitch, int radius, int d_lo, int d_hi,
-                                                        uint16_t* __restrict__ V) {
-    const int c = blockIdx.x * kWT + threadIdx.x;
-    const int d = d_lo + blockIdx.y;
-    if (c >= W || d >= d_hi) return;
-    uint16_t* Vd = V + (int64_t)(d - d_lo) * H * W + c;
-    if (c < d) {   // every AD of this column is 0 (Device.cu:27-31 + the memset)
-        for (int y = 0; y < H; ++y) Vd[(int64_t)y * W] = 0;
-        return;
+using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// |L - R| of 4 bytes as two packed-u16 pairs: even bytes (columns 0, 2) and odd bytes (1, 3)
+__device__ __forceinline__ void ad4(uint32_t l, uint32_t r, u16x2& e, u16x2& o) {
+    const u16x2 le = as_u16x2(__builtin_amdgcn_perm(0u, l, 0x0c020c00u)), lo = as_u16x2(__builtin_amdgcn_perm(0u, l, 0x0c030c01u));
+    const u16x2 re = as_u16x2(__builtin_amdgcn_perm(0u, r, 0x0c020c00u)), ro = as_u16x2(__builtin_amdgcn_perm(0u, r, 0x0c030c01u));
+    e = __builtin_elementwise_max(le, re) - __builtin_elementwise_min(le, re);
+    o = __builtin_elementwise_max(lo, ro) - __builtin_elementwise_min(lo, ro);
+}
+
+constexpr int kVT = 64;   // one wave per block: 256 columns
+
+// Columns c4..c4+3 of one d plane, rows [y0, y1).  L and R are read as one (possibly unaligned) dword per row
+// at a column clamped into [0, W - 4] and shifted back to c4 (resp. c4 - d) by a per-lane byte shift; the
+// keep-masks then zero the columns < d (Device.cu:27-31 + the memset) and >= W, whatever bytes the clamp read.
+// No lane takes a byte-load path (a wave straddling c = d costs what any other wave costs).
+__device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R, int W, int H,
+                                          int pitch, int radius, int d, int c4, int y0, int y1,
+                                          uint16_t* __restrict__ Vd) {
+    // per pair (even: columns 0, 2; odd: 1, 3; low half first) the columns kept
+    uint32_t keep_e = 0, keep_o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = (c4 + j >= d && c4 + j < W) ? 0xFFFFu << (16 * (j >> 1)) : 0u;
+        if (j & 1) keep_o |= m; else keep_e |= m;
     }
-    const uint8_t* lc = L + c;
-    const uint8_t* rc = R + c - d;
-    auto ad = [&](int y) -> uint32_t {
-        const int v = (int)lc[(int64_t)y * pitch] - (int)rc[(int64_t)y * pitch];
-        return (uint32_t)(v < 0 ? -v : v);
+    const int xl = min(c4, W - 4), xr = min(max(c4 - d, 0), W - 4);
+    const uint32_t shl = 8u * (uint32_t)(c4 - xl);                         // 0..3 bytes right
+    const int dr = c4 - d - xr;                                           // > 0: right edge, < 0: left of R's column 0
+    const uint32_t shr_r = 8u * (uint32_t)max(dr, 0), shl_r = 8u * (uint32_t)min(max(-dr, 0), 3);
+    auto row4 = [&](int y, uint32_t& l, uint32_t& r) {
+        const uint8_t* lr = L + (int64_t)y * pitch;
+        const uint8_t* rr = R + (int64_t)y * pitch;
+        __builtin_memcpy(&l, lr + xl, 4);
+        __builtin_memcpy(&r, rr + xr, 4);
+        l >>= shl;
+        r = (r >> shr_r) << shl_r;
     };
-    uint32_t s = 0;
-    const int y0e = min(radius, H - 1);
-    for (int y = 0; y <= y0e; ++y) s += ad(y);
-    // rows in blocks of kU: the kU entering and kU leaving rows of a block are loaded before the running sum
-    // consumes them (the loads of one row are independent of s), so their latencies overlap
+    u16x2 se = {0, 0}, so = {0, 0};
+    const int ps = max(y0 - radius, 0), pe = min(y0 + radius, H - 1);   // the window of row y0
+    for (int y = ps; y <= pe; y += 8) {
+        uint32_t l8[8], r8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) row4(min(y + k, pe), l8[k], r8[k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u16x2 e, o;
+            ad4(l8[k], r8[k], e, o);
+            const u16x2 z = {0, 0};
+            se += y + k <= pe ? e : z;
+            so += y + k <= pe ? o : z;
+        }
+    }
+    se = as_u16x2(as_u32(se) & keep_e);
+    so = as_u16x2(as_u32(so) & keep_o);
+    const bool full = c4 + 4 <= W;
     constexpr int kU = 8;
-    int y = 0;
-    for (; y + kU <= H; y += kU) {
-        uint32_t ain[kU], aout[kU];
+    int y = y0;
+    for (; y < y1; y += kU) {
+        // the kU entering and kU leaving rows, clamped into the frame and masked after: 4 kU loads in flight
+        uint32_t la[kU], ra[kU], lb[kU], rb[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-            const int ya = y + k + radius + 1, yb = y + k - radius;
-            ain[k] = ya < H ? ad(ya) : 0u;
-            aout[k] = yb >= 0 ? ad(yb) : 0u;
+            row4(min(y + k + radius + 1, H - 1), la[k], ra[k]);
+            row4(max(y + k - radius, 0), lb[k], rb[k]);
         }
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-            Vd[(int64_t)(y + k) * W] = (uint16_t)s;
-            s += ain[k];
-            s -= aout[k];
+            if (y + k < y1) {
+                // output columns c4..c4+3 = se.x, so.x, se.y, so.y
+                const uint32_t v01 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x05040100u);
+                const uint32_t v23 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x07060302u);
+                uint16_t* dst = Vd + (int64_t)(y + k) * W + c4;
+                if (full) {
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(v01, v23);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (c4 + j < W) dst[j] = (uint16_t)((j < 2 ? v01 : v23) >> (16 * (j & 1)));
+                }
+            }
+            u16x2 ei, oi, eo, oo;
+            ad4(la[k], ra[k], ei, oi);
+            ad4(lb[k], rb[k], eo, oo);
+            const uint32_t mi = y + k + radius + 1 < H ? 0xFFFFFFFFu : 0u, mo = y + k - radius >= 0 ? 0xFFFFFFFFu : 0u;
+            se = se + as_u16x2(as_u32(ei) & mi & keep_e);
+            so = so + as_u16x2(as_u32(oi) & mi & keep_o);
+            se = se - as_u16x2(as_u32(eo) & mo & keep_e);
+            so = so - as_u16x2(as_u32(oo) & mo & keep_o);
         }
     }
-    for (; y < H; ++y) {
-        Vd[(int64_t)y * W] = (uint16_t)s;
-        const int ya = y + radius + 1, yb = y - radius;
-        if (ya < H) s += ad(ya);
-        if (yb >= 0) s -= ad(yb);
-    }
+}
+
+// grid (ceil(W / 256), d_hi - d_lo, row chunks), one wave per block; V <= 255 * 255 so the packed u16 running
+// sums are exact (wrap-around in the intermediate add/sub cancels).
+__global__ __launch_bounds__(kVT) void wide_vsum_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
+                                                        int W, int H, int pitch, int radius, int d_lo, int d_hi,
+                                                        int chunk, uint16_t* __restrict__ V) {
+    const int c4 = (blockIdx.x * kVT + threadIdx.x) * 4;
+    const int d = d_lo + blockIdx.y;
+    const int y0 = blockIdx.z * chunk, y1 = min(y0 + chunk, H);
+    if (c4 >= W || d >= d_hi || y0 >= H) return;
+    uint16_t* Vd = V + (int64_t)(d - d_lo) * H * W;
+    vsum_walk(L, R, W, H, pitch, radius, d, c4, y0, y1, Vd);
 }
 
 // NPT outputs per thread (W <= 256 * NPT), contiguous: x in [8t, 8t + 8) for NPT 8.  The prefix row lives in LDS
@@ -182,14 +244,24 @@ size_t wide_workspace_bytes(int W, int H, int D) { return (size_t)D * W * H * si
 
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s) {
-    if (a.W <= 0 || a.H <= 0 || a.W > 4096 || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
+    if (a.W < 4 || a.H <= 0 || a.W > 4096 || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
         return hipErrorInvalidValue;
     const int nd = a.d_hi - a.d_lo;
+    // row chunks: enough waves to fill the chip (~32 per CU), each chunk at least a window tall (its prologue
+    // re-reads the 2r + 1 rows above it, from L2)
+    const unsigned gx = (unsigned)((a.W + 4 * kVT - 1) / (4 * kVT));
+#ifdef WIDE_X_NOCHUNK
+    const int want = 1;
+#else
+    const int want = std::max(1, (int)((8192 + gx * nd - 1) / (gx * nd)));
+#endif
+    const int chunk = std::max({(a.H + want - 1) / want, 2 * a.radius + 1, 32});
+    const int nch = (a.H + chunk - 1) / chunk;
     for (int f = 0; f < batch; ++f) {
         const uint8_t* Lf = a.left + (int64_t)f * a.frame_stride;
         const uint8_t* Rf = a.right + (int64_t)f * a.frame_stride;
-        hipLaunchKernelGGL(wide_vsum_kernel, dim3((unsigned)((a.W + kWT - 1) / kWT), (unsigned)nd), dim3(kWT), 0, s, Lf,
-                           Rf, a.W, a.H, a.pitch, a.radius, a.d_lo, a.d_hi, ws);
+        hipLaunchKernelGGL(wide_vsum_kernel, dim3(gx, (unsigned)nd, (unsigned)nch), dim3(kVT), 0, s, Lf, Rf, a.W, a.H,
+                           a.pitch, a.radius, a.d_lo, a.d_hi, chunk, ws);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         uint8_t* disp = a.disp ? a.disp + (int64_t)f * a.out_frame_stride : nullptr;
