@@ -3,14 +3,16 @@
 // 64-column tile keeps TW = 64 - 2r output columns, which vanishes as r grows.  Here the window sum is
 // separable through HBM, so a (pixel, d) costs the same at any radius:
 //   wide_vsum_kernel : V_d(y, c) = sum of AD_d over rows y-r..y+r (clipped), AD_d(y, c) = |L(y,c) - R(y,c-d)|
-//                      for c >= d else 0 (Device.cu:27-31); one thread per column walks the rows with a
-//                      running sum, one d per block column, u16 planes (V <= 255 * 255 = 65025).
-//   wide_hwta_kernel : one block per image row: per d the row of V is prefix-summed across the block (local
-//                      prefix + wave scan + 4-wave offsets), each output's window sum is two prefix reads,
-//                      and the key (S << 8 | d) is min-folded in registers with the validity d <= W - x
-//                      (Device.cu:44) and the 50 win^2 seed (:37).  The right view's candidate for u = x - d
-//                      (C_R(u, d) = C_L(u + d, d), StereoHelper.cpp:156-180) is min-folded into an LDS row
-//                      as well, so LR needs no second pass: the row is complete when the d loop ends.
+//                      for c >= d else 0 (Device.cu:27-31); one lane per 4 columns walks a chunk of rows with
+//                      packed-u16 running sums (V <= 255 * 255 = 65025), 8 rows' dword loads in flight at a
+//                      time, one d per block row; u16 planes written 8 B per lane per row.
+//   wide_hwta_kernel : one 256-lane block per image row: per d the row of V (prefetched one d ahead) is
+//                      prefix-summed across the block (local prefix + DPP wave scan + 4-wave offsets) into LDS,
+//                      each output's window sum is two prefix reads, and the key (S << 8 | d) is min-folded in
+//                      registers with the validity d <= W - x (Device.cu:44) and the 50 win^2 seed (:37).  The
+//                      right view's candidate for u = x - d (C_R(u, d) = C_L(u + d, d), StereoHelper.cpp:
+//                      156-180) is folded into an LDS row by atomic min, so LR needs no second pass.
+// HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R come from L2.
 // Exact integer arithmetic throughout: S <= 255 * 255^2 < 2^24, prefix sums < 4096 * 65025 < 2^32.
 #include <algorithm>
 
@@ -18,8 +20,6 @@
 
 namespace sm {
 namespace {
-
-constexpr int kWT = 256;
 
 using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
 
@@ -32,6 +32,18 @@ __device__ __forceinline__ void ad4(uint32_t l, uint32_t r, u16x2& e, u16x2& o) 
     const u16x2 re = as_u16x2(__builtin_amdgcn_perm(0u, r, 0x0c020c00u)), ro = as_u16x2(__builtin_amdgcn_perm(0u, r, 0x0c030c01u));
     e = __builtin_elementwise_max(le, re) - __builtin_elementwise_min(le, re);
     o = __builtin_elementwise_max(lo, ro) - __builtin_elementwise_min(lo, ro);
+}
+
+// Inclusive prefix sum over the 64 lanes with DPP moves (no LDS round trip): row_shr 1/2/4/8 scans each
+// 16-lane row, row_bcast:15 and :31 carry the rows' totals (disabled lanes read 0 through `old`).
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
 }
 
 constexpr int kVT = 64;   // one wave per block: 256 columns
@@ -133,17 +145,18 @@ __global__ __launch_bounds__(kVT) void wide_vsum_kernel(const uint8_t* __restric
 // NPT outputs per thread (W <= 256 * NPT), contiguous: x in [8t, 8t + 8) for NPT 8.  The prefix row lives in LDS
 // with one pad dword after every 8 (index i -> i + i / 8), so the 64 lanes' segment stores and their window
 // reads (lanes 9 dwords apart) fall on distinct banks.  Dynamic LDS: pref[2][NPAD] u32 (double-buffered over
-// d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.
-template <int NPT>
-__global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restrict__ V, int W, int H, int radius,
+// d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.  (Two d per
+// barrier pair, DP = 2, measured 7-20 % slower: profiles/microbench/r05_wide_path.txt.)
+template <int NPT, int NT>
+__global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restrict__ V, int W, int H, int radius,
                                                         int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
                                                         uint8_t* __restrict__ disp, int opitch,
                                                         uint32_t* __restrict__ keys, uint8_t* __restrict__ right,
                                                         int rpitch) {
     extern __shared__ __attribute__((aligned(16))) uint32_t wl[];
-    constexpr int NX = kWT * NPT + 1;                 // prefix entries 0..256 NPT
+    constexpr int NX = NT * NPT + 1;                  // prefix entries 0..NT NPT
     constexpr int NPAD = NX + NX / 8 + 1;
-    __shared__ uint32_t wsum[2][kWT / 64];
+    __shared__ uint32_t wsum[2][NT / 64];
     uint32_t* rmin = wl + 2 * NPAD;
     auto pad = [](int i) { return i + (i >> 3); };
     const int y = blockIdx.x;
@@ -151,7 +164,7 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
     const int x0 = t * NPT;
     const bool want_right = right != nullptr;
     if (want_right)
-        for (int i = t; i < NPAD; i += kWT) rmin[i] = 0xFFFFFFFFu;   // indexed pad(u), as pref
+        for (int i = t; i < NPAD; i += NT) rmin[i] = 0xFFFFFFFFu;   // indexed pad(u), as pref
     uint32_t best[NPT];
     int lo[NPT], hi[NPT];
 #pragma unroll
@@ -161,58 +174,82 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
         lo[k] = pad(max(x - radius, 0));              // window columns [lo, hi) of the prefix (Device.cu:51)
         hi[k] = pad(min(x + radius, W - 1) + 1);
     }
-    const bool vec = (W % 8) == 0 && (NPT % 8) == 0;   // 16-B rows: 8 u16 per load
-    for (int d = d_lo; d < d_hi; ++d) {
-        const int b = (d - d_lo) & 1;
-        uint32_t* pref = wl + b * NPAD;
+    // a row of V as NPT / 2 packed u16 pairs: 16-B loads (8-B at NPT 4) when W is a multiple of the chunk
+    constexpr int CH = NPT < 8 ? NPT : 8;
+    const bool vec = (W % CH) == 0;
+    auto load_row = [&](int d, uint32_t* raw) {
         const uint16_t* row = V + ((int64_t)(d - d_lo) * H + y) * W;
-        uint32_t p[NPT];
-        uint32_t acc = 0;
         if (vec) {
 #pragma unroll
-            for (int k = 0; k < NPT; k += 8) {
-                uint4 q = make_uint4(0, 0, 0, 0);
-                if (x0 + k < W) q = *reinterpret_cast<const uint4*>(row + x0 + k);
-                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc += w4[j] & 0xFFFFu;
-                    p[k + 2 * j] = acc;
-                    acc += w4[j] >> 16;
-                    p[k + 2 * j + 1] = acc;
+            for (int k = 0; k < NPT; k += CH) {
+                if constexpr (CH == 8) {
+                    uint4 q = make_uint4(0, 0, 0, 0);
+                    if (x0 + k < W) q = *reinterpret_cast<const uint4*>(row + x0 + k);
+                    raw[k / 2] = q.x; raw[k / 2 + 1] = q.y; raw[k / 2 + 2] = q.z; raw[k / 2 + 3] = q.w;
+                } else {
+                    uint2 q = make_uint2(0, 0);
+                    if (x0 + k < W) q = *reinterpret_cast<const uint2*>(row + x0 + k);
+                    raw[k / 2] = q.x; raw[k / 2 + 1] = q.y;
                 }
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                acc += x0 + k < W ? (uint32_t)row[x0 + k] : 0u;
-                p[k] = acc;
+            for (int k = 0; k < NPT; k += 2) {
+                const uint32_t v0 = x0 + k < W ? (uint32_t)row[x0 + k] : 0u;
+                const uint32_t v1 = x0 + k + 1 < W ? (uint32_t)row[x0 + k + 1] : 0u;
+                raw[k / 2] = v0 | v1 << 16;
             }
         }
-        // inclusive scan of the per-thread totals across the wave, then the waves' offsets
-        uint32_t inc = acc;
+    };
+    // the next d's row is loaded while this d's is scanned and folded: its HBM latency off the d loop's path
+    uint32_t nxt[NPT / 2];
+    load_row(d_lo, nxt);
+    for (int d = d_lo; d < d_hi; ++d) {
+        const int b = (d - d_lo) & 1;
+        uint32_t* pref = wl + b * NPAD;
+        uint32_t raw[NPT / 2];
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t n = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += n;
+        for (int k = 0; k < NPT / 2; ++k) raw[k] = nxt[k];
+        if (d + 1 < d_hi) load_row(d + 1, nxt);
+        uint32_t p[NPT];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < NPT / 2; ++k) {
+            acc += raw[k] & 0xFFFFu;
+            p[2 * k] = acc;
+            acc += raw[k] >> 16;
+            p[2 * k + 1] = acc;
         }
+        // inclusive scan of the per-thread totals across the wave, then the waves' offsets
+        const uint32_t inc = wave_inclusive_scan(acc);
         if (lane == 63) wsum[b][wv] = inc;
         __syncthreads();
         uint32_t base = inc - acc;
 #pragma unroll
-        for (int w = 0; w < kWT / 64; ++w) base += w < wv ? wsum[b][w] : 0u;
+        for (int w = 0; w < NT / 64; ++w) base += w < wv ? wsum[b][w] : 0u;
         if (t == 0) pref[0] = 0u;
 #pragma unroll
         for (int k = 0; k < NPT; ++k) pref[pad(x0 + k + 1)] = base + p[k];
         __syncthreads();
         const uint32_t dd = (uint32_t)(d & 0xFF);
+        // branch-free: columns x >= W fold garbage into best (never stored); the right view's fold is an LDS
+        // atomic min (no read-back), neutral 0xFFFFFFFF on the lane's own slot when x < d or x >= W
+        uint32_t key[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) key[k] = ((pref[hi[k]] - pref[lo[k]]) << 8) | dd;
+        if (x0 + NPT - 1 <= W - d) {   // every column of the thread valid at d (all but one wave)
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) best[k] = min(best[k], key[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) best[k] = d <= W - x0 - k ? min(best[k], key[k]) : best[k];   // Device.cu:44
+        }
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const int x = x0 + k;
-            if (x < W) {
-                const uint32_t key = ((pref[hi[k]] - pref[lo[k]]) << 8) | dd;
-                if (d <= W - x) best[k] = min(best[k], key);       // Device.cu:44
-                if (want_right && x >= d) rmin[pad(x - d)] = min(rmin[pad(x - d)], key);
+            if (want_right) {
+                const bool ok = x >= d && x < W;
+                atomicMin(&rmin[pad(ok ? x - d : x)], ok ? key[k] : 0xFFFFFFFFu);
             }
         }
     }
@@ -228,14 +265,23 @@ __global__ __launch_bounds__(kWT) void wide_hwta_kernel(const uint16_t* __restri
     }
 }
 
-template <int NPT>
+template <int NPT, int NT>
 hipError_t launch_h(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
                     uint8_t* disp, int opitch, uint32_t* keys, uint8_t* right, int rpitch, hipStream_t s) {
-    constexpr int NX = kWT * NPT + 1;
+    constexpr int NX = NT * NPT + 1;
     const size_t lds = (size_t)((right ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
-    hipLaunchKernelGGL(wide_hwta_kernel<NPT>, dim3((unsigned)H), dim3(kWT), lds, s, V, W, H, radius, d_lo, d_hi, seed,
-                       thresh, disp, opitch, keys, right, rpitch);
+    hipLaunchKernelGGL((wide_hwta_kernel<NPT, NT>), dim3((unsigned)H), dim3(NT), lds, s, V, W, H, radius, d_lo, d_hi,
+                       seed, thresh, disp, opitch, keys, right, rpitch);
     return hipGetLastError();
+}
+
+// 256 threads per row block, NPT = span / 256 outputs each (512- and 1024-thread blocks measured 20 % / 65 %
+// slower, 128-thread blocks 13 %: profiles/microbench/r05_wide_path.txt)
+template <int SPAN>
+hipError_t launch_span(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
+                       uint8_t* disp, int opitch, uint32_t* keys, uint8_t* right, int rpitch, hipStream_t s) {
+    constexpr int NPT = SPAN / 256;
+    return launch_h<NPT, 256>(V, W, H, radius, d_lo, d_hi, seed, thresh, disp, opitch, keys, right, rpitch, s);
 }
 
 }  // namespace
@@ -250,11 +296,7 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
     // row chunks: enough waves to fill the chip (~32 per CU), each chunk at least a window tall (its prologue
     // re-reads the 2r + 1 rows above it, from L2)
     const unsigned gx = (unsigned)((a.W + 4 * kVT - 1) / (4 * kVT));
-#ifdef WIDE_X_NOCHUNK
-    const int want = 1;
-#else
     const int want = std::max(1, (int)((8192 + gx * nd - 1) / (gx * nd)));
-#endif
     const int chunk = std::max({(a.H + want - 1) / want, 2 * a.radius + 1, 32});
     const int nch = (a.H + chunk - 1) / chunk;
     for (int f = 0; f < batch; ++f) {
@@ -267,15 +309,15 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
         uint8_t* disp = a.disp ? a.disp + (int64_t)f * a.out_frame_stride : nullptr;
         uint32_t* keys = a.keys ? a.keys + (int64_t)f * a.W * a.H : nullptr;
         uint8_t* rf = right ? right + (int64_t)f * rstride : nullptr;
-        if (a.W <= 4 * kWT)
-            e = launch_h<4>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys, rf,
-                            rpitch, s);
-        else if (a.W <= 8 * kWT)
-            e = launch_h<8>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys, rf,
-                            rpitch, s);
+        if (a.W <= 1024)
+            e = launch_span<1024>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
+                                  rf, rpitch, s);
+        else if (a.W <= 2048)
+            e = launch_span<2048>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
+                                  rf, rpitch, s);
         else
-            e = launch_h<16>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
-                             rf, rpitch, s);
+            e = launch_span<4096>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
+                                  rf, rpitch, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
