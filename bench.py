@@ -159,11 +159,14 @@ VARIANTS = (
     ("cfg3 1080p 11x11 guided d128", 1920, 1080, 128, 5, "guided", False, False, 32),
     ("cfg3 1080p 11x11 guided+lr d128", 1920, 1080, 128, 5, "guided", True, False, 32),
     ("cfg4 1080p 11x11 box d256", 1920, 1080, 256, 5, "box", False, False, 32),
-    # wide windows (the reference's SADWindowSize is unbounded, Device.cu:46-56): r 8..15 on the fused kernel
+    # wide windows (the reference's SADWindowSize is unbounded, Device.cu:46-56): r 8..15 on the fused kernel,
     ("1080p 17x17 box d128", 1920, 1080, 128, 8, "box", False, False, 32),
     ("1080p 23x23 box d128", 1920, 1080, 128, 11, "box", False, False, 32),
     ("1080p 31x31 box d128", 1920, 1080, 128, 15, "box", False, False, 32),
     ("1080p 31x31 box+lr d128", 1920, 1080, 128, 15, "box", True, False, 32),
+    # r 16..127: the separable wide-window path (csrc/bm_wide.hip)
+    ("1080p 41x41 box d128", 1920, 1080, 128, 20, "box", False, False, 8),
+    ("1080p 255x255 box+lr d128", 1920, 1080, 128, 127, "box", True, False, 8),
     ("cfg5 4K 11x11 box d192", 3840, 2160, 192, 5, "box", False, False, 8),
     ("cfg5 4K 11x11 box+lr d192", 3840, 2160, 192, 5, "box", True, False, 8),
     ("cfg5 4K 11x11 guided+lr d192", 3840, 2160, 192, 5, "guided", True, False, 8),
