@@ -84,9 +84,9 @@ hipError_t launch_all_sad_generic(const uint8_t* L, const uint8_t* R, int W, int
 // (`frames` consecutive frames of D planes each; frame f's map at disp + f * out_stride)
 hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frames, uint32_t seed_key, uint8_t* disp,
                              int out_pitch, int64_t out_stride, hipStream_t s);
-// radius 16..127 (bm_wide.hip): V planes (u16, (d_hi - d_lo) * W * H in `ws`, wide_workspace_bytes) then one
-// block per image row; a.valid_mode 0, W <= 4096.  right (optional): the right view's dR [batch][H][rpitch]
-size_t wide_workspace_bytes(int W, int H, int D);
+// radius 16..127 (bm_wide.hip): V planes (u16, (d_hi - d_lo) * W * H per frame of a launch group, in `ws`,
+// wide_workspace_bytes) then one block per image row; a.valid_mode 0, 4 <= W <= 4096.  right (optional): the right view's dR [batch][H][rpitch]
+size_t wide_workspace_bytes(int W, int H, int D, int batch);
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s);
 constexpr int kMaxWideWidth = 4096;

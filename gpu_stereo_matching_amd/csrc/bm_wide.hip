@@ -15,13 +15,16 @@
 // HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R come from L2.
 // Exact integer arithmetic throughout: S <= 255 * 255^2 < 2^24, prefix sums < 4096 * 65025 < 2^32.
 #include <algorithm>
+#include <type_traits>
 
 #include "bm_common.h"
+
 
 namespace sm {
 namespace {
 
 using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -55,22 +58,28 @@ constexpr int kVT = 64;   // one wave per block: 256 columns
 __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R, int W, int H,
                                           int pitch, int radius, int d, int c4, int y0, int y1,
                                           uint16_t* __restrict__ Vd) {
-    // per pair (even: columns 0, 2; odd: 1, 3; low half first) the columns kept
-    uint32_t keep_e = 0, keep_o = 0;
+    // the columns kept, in output order (columns c4, c4 + 1 | c4 + 2, c4 + 3): the running sums of a
+    // column < d or >= W carry garbage (wrapping u16 arithmetic) and are zeroed at the store
+    uint32_t keep01 = 0, keep23 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint32_t m = (c4 + j >= d && c4 + j < W) ? 0xFFFFu << (16 * (j >> 1)) : 0u;
-        if (j & 1) keep_o |= m; else keep_e |= m;
+        const uint32_t m = (c4 + j >= d && c4 + j < W) ? 0xFFFFu << (16 * (j & 1)) : 0u;
+        if (j < 2) keep01 |= m; else keep23 |= m;
     }
     const int xl = min(c4, W - 4), xr = min(max(c4 - d, 0), W - 4);
     const uint32_t shl = 8u * (uint32_t)(c4 - xl);                         // 0..3 bytes right
     const int dr = c4 - d - xr;                                           // > 0: right edge, < 0: left of R's column 0
     const uint32_t shr_r = 8u * (uint32_t)max(dr, 0), shl_r = 8u * (uint32_t)min(max(-dr, 0), 3);
+    // buffer loads: the row offset is wave-uniform (SGPR soffset), the column a 32-bit lane offset, so a
+    // load needs no per-lane 64-bit address math (global loads spent a v_mad_i64_i32 per load); the frame
+    // bounds check of the descriptor returns 0 past the last row (never reached: rows are clamped)
+    const int nrec = pitch * H;
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(L), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(R), 0, nrec, 0x00020000);
     auto row4 = [&](int y, uint32_t& l, uint32_t& r) {
-        const uint8_t* lr = L + (int64_t)y * pitch;
-        const uint8_t* rr = R + (int64_t)y * pitch;
-        __builtin_memcpy(&l, lr + xl, 4);
-        __builtin_memcpy(&r, rr + xr, 4);
+        const int ro = y * pitch;
+        l = __builtin_amdgcn_raw_buffer_load_b32(rsl, xl, ro, 0);
+        r = __builtin_amdgcn_raw_buffer_load_b32(rsr, xr, ro, 0);
         l >>= shl;
         r = (r >> shr_r) << shl_r;
     };
@@ -89,28 +98,31 @@ __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const u
             so += y + k <= pe ? o : z;
         }
     }
-    se = as_u16x2(as_u32(se) & keep_e);
-    so = as_u16x2(as_u32(so) & keep_o);
     const bool full = c4 + 4 <= W;
     constexpr int kU = 8;
-    int y = y0;
-    for (; y < y1; y += kU) {
-        // the kU entering and kU leaving rows, clamped into the frame and masked after: 4 kU loads in flight
+    // one batch of kU rows: the kU entering and kU leaving rows, clamped into the frame, loaded together
+    // (4 kU loads in flight), then the sums; EDGE batches (a row entering past H or leaving above 0,
+    // wave-uniform) mask those rows' AD
+    auto batch = [&](int y, auto edge) {
+        constexpr bool EDGE = decltype(edge)::value;
         uint32_t la[kU], ra[kU], lb[kU], rb[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-            row4(min(y + k + radius + 1, H - 1), la[k], ra[k]);
-            row4(max(y + k - radius, 0), lb[k], rb[k]);
+            row4(EDGE ? min(y + k + radius + 1, H - 1) : y + k + radius + 1, la[k], ra[k]);
+            row4(EDGE ? max(y + k - radius, 0) : y + k - radius, lb[k], rb[k]);
         }
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-            if (y + k < y1) {
+            if (!EDGE || y + k < y1) {
                 // output columns c4..c4+3 = se.x, so.x, se.y, so.y
-                const uint32_t v01 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x05040100u);
-                const uint32_t v23 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x07060302u);
+                const uint32_t v01 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x05040100u) & keep01;
+                const uint32_t v23 = __builtin_amdgcn_perm(as_u32(so), as_u32(se), 0x07060302u) & keep23;
                 uint16_t* dst = Vd + (int64_t)(y + k) * W + c4;
                 if (full) {
-                    *reinterpret_cast<uint2*>(dst) = make_uint2(v01, v23);
+                    // nontemporal: the planes are streamed once each way (plain stores and loads measured
+                    // 8-13 % slower over both kernels)
+                    __builtin_nontemporal_store(v01, reinterpret_cast<uint32_t*>(dst));
+                    __builtin_nontemporal_store(v23, reinterpret_cast<uint32_t*>(dst) + 1);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
@@ -120,25 +132,39 @@ __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const u
             u16x2 ei, oi, eo, oo;
             ad4(la[k], ra[k], ei, oi);
             ad4(lb[k], rb[k], eo, oo);
-            const uint32_t mi = y + k + radius + 1 < H ? 0xFFFFFFFFu : 0u, mo = y + k - radius >= 0 ? 0xFFFFFFFFu : 0u;
-            se = se + as_u16x2(as_u32(ei) & mi & keep_e);
-            so = so + as_u16x2(as_u32(oi) & mi & keep_o);
-            se = se - as_u16x2(as_u32(eo) & mo & keep_e);
-            so = so - as_u16x2(as_u32(oo) & mo & keep_o);
+            if (EDGE) {
+                const uint32_t mi = y + k + radius + 1 < H ? 0xFFFFFFFFu : 0u;
+                const uint32_t mo = y + k - radius >= 0 ? 0xFFFFFFFFu : 0u;
+                ei = as_u16x2(as_u32(ei) & mi);
+                oi = as_u16x2(as_u32(oi) & mi);
+                eo = as_u16x2(as_u32(eo) & mo);
+                oo = as_u16x2(as_u32(oo) & mo);
+            }
+            se = se + ei - eo;
+            so = so + oi - oo;
         }
+    };
+    for (int y = y0; y < y1; y += kU) {
+        if (y - radius >= 0 && y + kU + radius < H && y + kU <= y1)
+            batch(y, std::false_type{});
+        else
+            batch(y, std::true_type{});
     }
 }
 
-// grid (ceil(W / 256), d_hi - d_lo, row chunks), one wave per block; V <= 255 * 255 so the packed u16 running
-// sums are exact (wrap-around in the intermediate add/sub cancels).
+// grid (ceil(W / 256), d_hi - d_lo, row chunks x frames of the group), one wave per block; V <= 255 * 255 so
+// the packed u16 running sums are exact (wrap-around in the intermediate add/sub cancels).
 __global__ __launch_bounds__(kVT) void wide_vsum_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
-                                                        int W, int H, int pitch, int radius, int d_lo, int d_hi,
-                                                        int chunk, uint16_t* __restrict__ V) {
+                                                        int64_t fstride, int W, int H, int pitch, int radius, int d_lo,
+                                                        int d_hi, int chunk, int nch, uint16_t* __restrict__ V) {
     const int c4 = (blockIdx.x * kVT + threadIdx.x) * 4;
     const int d = d_lo + blockIdx.y;
-    const int y0 = blockIdx.z * chunk, y1 = min(y0 + chunk, H);
+    const int g = blockIdx.z / nch;
+    const int y0 = (blockIdx.z - g * nch) * chunk, y1 = min(y0 + chunk, H);
     if (c4 >= W || d >= d_hi || y0 >= H) return;
-    uint16_t* Vd = V + (int64_t)(d - d_lo) * H * W;
+    L += g * fstride;
+    R += g * fstride;
+    uint16_t* Vd = V + ((int64_t)g * (d_hi - d_lo) + (d - d_lo)) * H * W;
     vsum_walk(L, R, W, H, pitch, radius, d, c4, y0, y1, Vd);
 }
 
@@ -147,19 +173,33 @@ __global__ __launch_bounds__(kVT) void wide_vsum_kernel(const uint8_t* __restric
 // reads (lanes 9 dwords apart) fall on distinct banks.  Dynamic LDS: pref[2][NPAD] u32 (double-buffered over
 // d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.  (Two d per
 // barrier pair, DP = 2, measured 7-20 % slower: profiles/microbench/r05_wide_path.txt.)
+struct WideOut {
+    uint8_t* disp;    // left map (or null), out_pitch / out_frame_stride
+    int opitch;
+    int64_t ofs;
+    uint32_t* keys;   // raw keys [frame][H][W] (or null)
+    uint8_t* right;   // right view (or null)
+    int rpitch;
+    int64_t rfs;
+};
+
+// grid (H, frames of the group)
 template <int NPT, int NT>
 __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restrict__ V, int W, int H, int radius,
                                                         int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
-                                                        uint8_t* __restrict__ disp, int opitch,
-                                                        uint32_t* __restrict__ keys, uint8_t* __restrict__ right,
-                                                        int rpitch) {
+                                                        WideOut out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t wl[];
     constexpr int NX = NT * NPT + 1;                  // prefix entries 0..NT NPT
     constexpr int NPAD = NX + NX / 8 + 1;
     __shared__ uint32_t wsum[2][NT / 64];
     uint32_t* rmin = wl + 2 * NPAD;
     auto pad = [](int i) { return i + (i >> 3); };
-    const int y = blockIdx.x;
+    const int y = blockIdx.x, g = blockIdx.y;
+    V += (int64_t)g * (d_hi - d_lo) * H * W;
+    uint8_t* __restrict__ disp = out.disp ? out.disp + g * out.ofs : nullptr;
+    uint32_t* __restrict__ keys = out.keys ? out.keys + (int64_t)g * W * H : nullptr;
+    uint8_t* __restrict__ right = out.right ? out.right + g * out.rfs : nullptr;
+    const int opitch = out.opitch, rpitch = out.rpitch;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int x0 = t * NPT;
     const bool want_right = right != nullptr;
@@ -167,10 +207,13 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
         for (int i = t; i < NPAD; i += NT) rmin[i] = 0xFFFFFFFFu;   // indexed pad(u), as pref
     uint32_t best[NPT];
     int lo[NPT], hi[NPT];
+    bool xin[NPT];
+    const int p0 = pad(x0);
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         best[k] = seed;
         const int x = x0 + k;
+        xin[k] = x < W;
         lo[k] = pad(max(x - radius, 0));              // window columns [lo, hi) of the prefix (Device.cu:51)
         hi[k] = pad(min(x + radius, W - 1) + 1);
     }
@@ -183,8 +226,8 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
 #pragma unroll
             for (int k = 0; k < NPT; k += CH) {
                 if constexpr (CH == 8) {
-                    uint4 q = make_uint4(0, 0, 0, 0);
-                    if (x0 + k < W) q = *reinterpret_cast<const uint4*>(row + x0 + k);
+                    u32x4 q = {0u, 0u, 0u, 0u};
+                    if (x0 + k < W) q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + x0 + k));
                     raw[k / 2] = q.x; raw[k / 2 + 1] = q.y; raw[k / 2 + 2] = q.z; raw[k / 2 + 3] = q.w;
                 } else {
                     uint2 q = make_uint2(0, 0);
@@ -202,6 +245,7 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
         }
     };
     // the next d's row is loaded while this d's is scanned and folded: its HBM latency off the d loop's path
+    // (two d ahead measured the same: profiles/microbench/r05_wide_path.txt)
     uint32_t nxt[NPT / 2];
     load_row(d_lo, nxt);
     for (int d = d_lo; d < d_hi; ++d) {
@@ -244,12 +288,18 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
 #pragma unroll
             for (int k = 0; k < NPT; ++k) best[k] = d <= W - x0 - k ? min(best[k], key[k]) : best[k];   // Device.cu:44
         }
+        if (want_right) {
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const int x = x0 + k;
-            if (want_right) {
-                const bool ok = x >= d && x < W;
-                atomicMin(&rmin[pad(ok ? x - d : x)], ok ? key[k] : 0xFFFFFFFFu);
+            for (int k = 0; k < NPT; ++k) {
+                const bool ok = x0 + k >= d && xin[k];
+                if constexpr (NPT % 8 == 0) {
+                    // x0 a multiple of 8: pad(x - d) = pad(x0) + (k - d) + ((k - d) >> 3), one lane constant
+                    // plus a wave-uniform part
+                    const int off = ok ? (k - d) + ((k - d) >> 3) : k + (k >> 3);
+                    atomicMin(&rmin[p0 + off], ok ? key[k] : 0xFFFFFFFFu);
+                } else {
+                    atomicMin(&rmin[pad(ok ? x0 + k - d : x0 + k)], ok ? key[k] : 0xFFFFFFFFu);
+                }
             }
         }
     }
@@ -267,11 +317,11 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
 
 template <int NPT, int NT>
 hipError_t launch_h(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
-                    uint8_t* disp, int opitch, uint32_t* keys, uint8_t* right, int rpitch, hipStream_t s) {
+                    const WideOut& out, int frames, hipStream_t s) {
     constexpr int NX = NT * NPT + 1;
-    const size_t lds = (size_t)((right ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
-    hipLaunchKernelGGL((wide_hwta_kernel<NPT, NT>), dim3((unsigned)H), dim3(NT), lds, s, V, W, H, radius, d_lo, d_hi,
-                       seed, thresh, disp, opitch, keys, right, rpitch);
+    const size_t lds = (size_t)((out.right ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
+    hipLaunchKernelGGL((wide_hwta_kernel<NPT, NT>), dim3((unsigned)H, (unsigned)frames), dim3(NT), lds, s, V, W, H,
+                       radius, d_lo, d_hi, seed, thresh, out);
     return hipGetLastError();
 }
 
@@ -279,45 +329,58 @@ hipError_t launch_h(const uint16_t* V, int W, int H, int radius, int d_lo, int d
 // slower, 128-thread blocks 13 %: profiles/microbench/r05_wide_path.txt)
 template <int SPAN>
 hipError_t launch_span(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
-                       uint8_t* disp, int opitch, uint32_t* keys, uint8_t* right, int rpitch, hipStream_t s) {
+                       const WideOut& out, int frames, hipStream_t s) {
     constexpr int NPT = SPAN / 256;
-    return launch_h<NPT, 256>(V, W, H, radius, d_lo, d_hi, seed, thresh, disp, opitch, keys, right, rpitch, s);
+    return launch_h<NPT, 256>(V, W, H, radius, d_lo, d_hi, seed, thresh, out, frames, s);
+}
+
+// frames per vsum / hwta launch pair: enough row blocks for ~8 per CU (1080 rows of one 1080p frame give 4);
+// 1080p: 2 frames per pair measured 7-8 % faster than 1, 4 the same as 2
+int wide_group(int H, int batch) {
+    const int want = (2048 + H - 1) / H;
+    return std::max(1, std::min({want, batch, 4}));
 }
 
 }  // namespace
 
-size_t wide_workspace_bytes(int W, int H, int D) { return (size_t)D * W * H * sizeof(uint16_t); }
+size_t wide_workspace_bytes(int W, int H, int D, int batch) {
+    return (size_t)wide_group(H, batch) * D * W * H * sizeof(uint16_t);
+}
 
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s) {
     if (a.W < 4 || a.H <= 0 || a.W > 4096 || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
         return hipErrorInvalidValue;
     const int nd = a.d_hi - a.d_lo;
+    const int G = wide_group(a.H, batch);
     // row chunks: enough waves to fill the chip (~32 per CU), each chunk at least a window tall (its prologue
     // re-reads the 2r + 1 rows above it, from L2)
     const unsigned gx = (unsigned)((a.W + 4 * kVT - 1) / (4 * kVT));
-    const int want = std::max(1, (int)((8192 + gx * nd - 1) / (gx * nd)));
+    const int64_t waves = (int64_t)gx * nd * G;
+    const int want = (int)std::max<int64_t>(1, (8192 + waves - 1) / waves);
     const int chunk = std::max({(a.H + want - 1) / want, 2 * a.radius + 1, 32});
     const int nch = (a.H + chunk - 1) / chunk;
-    for (int f = 0; f < batch; ++f) {
-        const uint8_t* Lf = a.left + (int64_t)f * a.frame_stride;
-        const uint8_t* Rf = a.right + (int64_t)f * a.frame_stride;
-        hipLaunchKernelGGL(wide_vsum_kernel, dim3(gx, (unsigned)nd, (unsigned)nch), dim3(kVT), 0, s, Lf, Rf, a.W, a.H,
-                           a.pitch, a.radius, a.d_lo, a.d_hi, chunk, ws);
+    for (int f = 0; f < batch; f += G) {
+        const int n = std::min(G, batch - f);
+        hipLaunchKernelGGL(wide_vsum_kernel, dim3(gx, (unsigned)nd, (unsigned)(nch * n)), dim3(kVT), 0, s,
+                           a.left + (int64_t)f * a.frame_stride, a.right + (int64_t)f * a.frame_stride, a.frame_stride,
+                           a.W, a.H, a.pitch, a.radius, a.d_lo, a.d_hi, chunk, nch, ws);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        uint8_t* disp = a.disp ? a.disp + (int64_t)f * a.out_frame_stride : nullptr;
-        uint32_t* keys = a.keys ? a.keys + (int64_t)f * a.W * a.H : nullptr;
-        uint8_t* rf = right ? right + (int64_t)f * rstride : nullptr;
+        WideOut out;
+        out.disp = a.disp ? a.disp + (int64_t)f * a.out_frame_stride : nullptr;
+        out.opitch = a.out_pitch;
+        out.ofs = a.out_frame_stride;
+        out.keys = a.keys ? a.keys + (int64_t)f * a.W * a.H : nullptr;
+        out.right = right ? right + (int64_t)f * rstride : nullptr;
+        out.rpitch = rpitch;
+        out.rfs = rstride;
         if (a.W <= 1024)
-            e = launch_span<1024>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
-                                  rf, rpitch, s);
+            e = launch_span<1024>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, out, n, s);
         else if (a.W <= 2048)
-            e = launch_span<2048>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
-                                  rf, rpitch, s);
+            e = launch_span<2048>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, out, n, s);
         else
-            e = launch_span<4096>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, disp, a.out_pitch, keys,
-                                  rf, rpitch, s);
+            e = launch_span<4096>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, out, n, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -325,7 +325,7 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
     } else if (wide) {
-        int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D));
+        int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D, batch));
         if (rc) return rc;
         SM_HIP(sm::launch_box_match_wide(a, batch, reinterpret_cast<uint16_t*>(h->d_vol), lr ? right_map : nullptr, W,
                                          P, s));
@@ -773,7 +773,7 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
     a.keys = keys;
     if (!rkeys) {
         if (sm::wide_path(radius, W)) {   // the wide-window path (bm_wide.hip)
-            int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo));
+            int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo, 1));
             if (rc) return rc;
             SM_HIP(sm::launch_box_match_wide(a, 1, reinterpret_cast<uint16_t*>(h->d_vol), nullptr, 0, 0, s));
             return SM_OK;
