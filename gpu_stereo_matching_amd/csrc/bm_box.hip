@@ -454,21 +454,32 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
     __syncthreads();
     uint8_t* Df = a.disp ? a.disp + (int64_t)frame * a.out_frame_stride : nullptr;
     uint32_t* Kf = a.keys ? a.keys + (int64_t)frame * W * H : nullptr;
-    for (int e = tid; e < kTileH * G::TW; e += kThreads) {
-        const int j = e / G::TW, o = e - j * G::TW;
-        const int y = y0 + j, x = x0 + o;
-        if (y >= H || x >= W) continue;
-        const uint32_t k = fold[e];
-        if (Df) Df[(int64_t)y * a.out_pitch + x] = k < a.thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
-        if (Kf) Kf[(int64_t)y * W + x] = k;
+    // lane = output column (TW <= 64), rows over the waves: no per-element division, wave-uniform row bases
+    if (lane < G::TW && x0 + lane < W) {
+        const int ylim = min(kTileH, H - y0);
+        uint8_t* drow = Df ? Df + (int64_t)y0 * a.out_pitch + x0 + lane : nullptr;
+        uint32_t* krow = Kf ? Kf + (int64_t)y0 * W + x0 + lane : nullptr;
+#pragma unroll
+        for (int j = wave; j < kTileH; j += NW) {
+            if (j >= ylim) break;
+            const uint32_t k = fold[j * G::TW + lane];
+            if (drow) drow[(int64_t)j * a.out_pitch] = k < a.thresh_key ? (uint8_t)(k & 0xFFu) : (uint8_t)0;
+            if (krow) krow[(int64_t)j * W] = k;
+        }
     }
     if constexpr (RIGHT) {
         // rb is untouched by the fold (which aliases the CS area); rows past H are never read
         uint32_t* P = a.rpart + (int64_t)tile_id * (kTileH * G::PWP);   // [frame][ty][tx][kTileH][PWP]
         const int lead = rr_lead(tx, G::TW, DMAX);
-        for (int e = tid; e < kTileH * G::PWP; e += kThreads) {
-            const int j = e / G::PWP, k = e - j * G::PWP - lead;
-            P[e] = (k >= 0 && k < G::PW) ? rb[G::rb_row(j) + k] : 0xFFFFFFFFu;
+        // rows over the waves, entries over the lanes (no per-element division)
+        for (int j = wave; j < kTileH; j += NW) {
+            uint32_t* prow = P + j * G::PWP;
+            const uint32_t* rrow = rb + G::rb_row(j) - lead;
+#pragma unroll
+            for (int e = lane; e < G::PWP; e += 64) {
+                const int k = e - lead;
+                prow[e] = (k >= 0 && k < G::PW) ? rrow[e] : 0xFFFFFFFFu;
+            }
         }
     }
 }
