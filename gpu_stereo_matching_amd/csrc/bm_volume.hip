@@ -31,21 +31,10 @@ constexpr int kVT = 256;
 #ifndef SM_ADV_ROWS
 #define SM_ADV_ROWS 2      // image rows per block
 #endif
-// Block order (round 4; profiles/microbench/r04_ad_order_ab.txt).  0 (default): the
-// grid (band, frame, chunk) in blockIdx (x, y, z): the blocks in flight write the 8 planes of one chunk
-// for ~8 frames, 64 long streams, but the chunks of one band run ~bands*frames blocks apart, so each
-// re-fetches the band from the fabric (rocprof FETCH 1.17x the algorithmic bytes at 16 chunks).
-// 1: one flat grid, the d chunk the fastest index and the ids remapped XCD-contiguously (xcd_tile): the
-// band is fetched once (1.0001x), but the blocks in flight write all D planes at once and the launch
-// runs 63 us per 1080p frame against 48 (HIP events, same box).
-// 2: chunk groups of SM_ADV_GC, the group's chunks fastest and XCD-contiguous, then the band, then the
-// group (GC 1 / 2 / 4: 54 / 59 / 59 us).  3: (band, chunk, frame), a band's chunks `bands` blocks apart.
-#ifndef SM_ADV_ORDER
-#define SM_ADV_ORDER 0
-#endif
-#ifndef SM_ADV_GC
-#define SM_ADV_GC 2
-#endif
+// Block order (round 4; profiles/microbench/r04_ad_order_ab.txt): the grid (band, frame,
+// chunk) in blockIdx (x, y, z), so the blocks in flight write the planes of one chunk for ~8 frames.  Measured
+// and removed in round 5 (git history): a flat d-fastest XCD-contiguous order (63 us per 1080p frame against
+// 48: every plane written at once), chunk groups (54-59 us) and (band, chunk, frame).
 
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -70,34 +59,12 @@ __device__ __forceinline__ uint32_t absdiff_u8x4(uint32_t a, uint32_t b) {
 template <int KF>
 __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                         int W, int H, int pitch, int64_t fstride, int D, int RB,
-                                                        int bands, int dsp, int gc, uint8_t* __restrict__ dif,
-                                                        int64_t dstride) {
+                                                        int dsp, uint8_t* __restrict__ dif, int64_t dstride) {
     constexpr int SEG = 16, NQ = 4;
     constexpr int kVPad = SEG;   // zero bytes in front of each staged R row (x - d down to -SEG)
     extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [RB][rstride]
-#if SM_ADV_ORDER == 2
-    // gc chunks per group (gc divides dsp): id = (group, band-frame, chunk in group)
-    const int id = xcd_tile(blockIdx.x, gridDim.x);
-    const int nbf = (int)(gridDim.x / (unsigned)dsp);
-    const int cl = id % gc, rest = id / gc;
-    const int bf = rest % nbf, dz = (rest / nbf) * gc + cl;
-    const int f = bf / bands, y0 = (bf - f * bands) * RB;
-#elif SM_ADV_ORDER == 3
-    // (band, chunk, frame): a band's chunks run `bands` blocks apart instead of bands * frames
-    const int y0 = blockIdx.x * RB, dz = blockIdx.y, f = blockIdx.z;
-    (void)bands;
-    (void)gc;
-#elif SM_ADV_ORDER
-    const int id = xcd_tile(blockIdx.x, gridDim.x);
-    const int dz = id % dsp, bf = id / dsp;
-    const int f = bf / bands, y0 = (bf - f * bands) * RB;
-    (void)gc;
-#else
     const int y0 = blockIdx.x * RB, f = blockIdx.y;
     const int dz = blockIdx.z;
-    (void)bands;
-    (void)gc;
-#endif
     const int dc = (D + dsp - 1) / dsp;                           // disparities of this block
     const int d_begin = dz * dc, d_end = d_begin + dc < D ? d_begin + dc : D;
     const int nseg = (W + SEG - 1) / SEG;
@@ -198,142 +165,13 @@ __global__ __launch_bounds__(kVT) void ad_volume_kernel(const uint8_t* __restric
     }
 }
 
-// Variant (round 5): each thread owns CS consecutive 16-B segments (CS * 16 contiguous
-// bytes of one row), so a wave's stores for one d cover CS KB of the plane in CS store instructions -- the
-// "16-B chunk 4/lane" pattern that streamed at 0.76 of 8 TB/s against 0.72 for one chunk per lane
-// (profiles/microbench/r03_hbm_write_patterns.txt).  Rows per block RB, d chunks as ad_volume_kernel.
-template <int CS>
-__global__ __launch_bounds__(kVT) void ad_volume_cs_kernel(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
-                                                           int W, int H, int pitch, int64_t fstride, int D, int RB,
-                                                           int dsp, uint8_t* __restrict__ dif, int64_t dstride) {
-    constexpr int SEG = 16, NQ = 4;
-    constexpr int kVPad = SEG;
-    extern __shared__ __attribute__((aligned(16))) uint8_t rrow[];   // [RB][rstride]
-    const int y0 = blockIdx.x * RB, f = blockIdx.y, dz = blockIdx.z;
-    const int dc = (D + dsp - 1) / dsp;
-    const int d_begin = dz * dc, d_end = d_begin + dc < D ? d_begin + dc : D;
-    const int nseg = (W + SEG - 1) / SEG;
-    const int ngrp = (nseg + CS - 1) / CS;                          // CS-segment groups per row
-    const int rdw = (kVPad + ngrp * CS * SEG + 4) / 4;              // staged dwords per R row
-    const int rows = min(RB, H - y0);
-    for (int e = threadIdx.x; e < rows * rdw; e += kVT) {
-        const int i = e / rdw, j = e - i * rdw;
-        const uint8_t* rr = R + (int64_t)f * fstride + (int64_t)(y0 + i) * pitch;
-        const int c = 4 * j - kVPad;
-        uint32_t v = 0;
-        if (c >= 0 && c + 3 < W) {
-            __builtin_memcpy(&v, rr + c, 4);
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (c + b >= 0 && c + b < W) v |= (uint32_t)rr[c + b] << (8 * b);
-        }
-        reinterpret_cast<uint32_t*>(rrow)[e] = v;
-    }
-    __syncthreads();
-    const int64_t P = (int64_t)W * H;
-    const int nflat = rows * ngrp;
-    const int fl = threadIdx.x;
-    if (fl >= nflat) return;
-    const int i = fl / ngrp;
-    const int x0 = (fl - i * ngrp) * CS * SEG;
-    uint8_t* out = dif + (int64_t)f * dstride + (int64_t)(y0 + i) * W + x0;   // + d * P
-    const bool vec = ((W & 15) == 0) && ((P & 15) == 0) && ((reinterpret_cast<uintptr_t>(dif) & 15) == 0) &&
-                     ((dstride & 15) == 0) && x0 + CS * SEG <= W;
-    uint32_t l[CS * NQ];
-    {
-        const uint8_t* lr = L + (int64_t)f * fstride + (int64_t)(y0 + i) * pitch + x0;
-#pragma unroll
-        for (int q = 0; q < CS * NQ; ++q) {
-            if (x0 + 4 * q + 3 < W) {
-                __builtin_memcpy(&l[q], lr + 4 * q, 4);
-            } else {
-                uint32_t v = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (x0 + 4 * q + b < W) v |= (uint32_t)lr[4 * q + b] << (8 * b);
-                l[q] = v;
-            }
-        }
-    }
-    const uint8_t* rbase = rrow + (size_t)i * rdw * 4;
-#pragma unroll 2
-    for (int d = d_begin; d < d_end; ++d) {
-        uint32_t r[CS * NQ];
-        const int start = kVPad + x0 - d;
-        if (start >= 0) {
-            const int base = start & ~3, sh = start & 3;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(rbase + base);
-            uint32_t wv[CS * NQ + 1];
-#pragma unroll
-            for (int q = 0; q <= CS * NQ; ++q) wv[q] = w[q];
-#pragma unroll
-            for (int q = 0; q < CS * NQ; ++q) r[q] = __builtin_amdgcn_alignbyte(wv[q + 1], wv[q], sh);
-        } else {   // x0 < d - 16: bytes below d are masked below; the rest read the padded row from its start
-#pragma unroll
-            for (int q = 0; q < CS * NQ; ++q) {
-                const int s2 = start + 4 * q;
-                uint32_t v = 0;
-                if (s2 >= 0) {
-                    const uint32_t* w = reinterpret_cast<const uint32_t*>(rbase + (s2 & ~3));
-                    v = __builtin_amdgcn_alignbyte(w[1], w[0], s2 & 3);
-                }
-                r[q] = v;
-            }
-        }
-        uint32_t o[CS * NQ];
-#pragma unroll
-        for (int q = 0; q < CS * NQ; ++q) o[q] = absdiff_u8x4(l[q], r[q]);
-        if (x0 < d + SEG * CS) {   // bytes with x < d are 0 (Device.cu:27-31 + the memset)
-#pragma unroll
-            for (int q = 0; q < CS * NQ; ++q) {
-                const int n = min(max(d - x0 - 4 * q, 0), 4);
-                o[q] &= (uint32_t)(~0ull << (8 * n));
-            }
-        }
-        uint8_t* dst = out + (int64_t)d * P;
-        if (vec) {
-#pragma unroll
-            for (int k = 0; k < CS; ++k) {
-                const u32x4 v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
-                if (SM_ADV_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst) + k);
-                else reinterpret_cast<u32x4*>(dst)[k] = v;
-            }
-        } else {
-            const int n = W - x0 < CS * SEG ? W - x0 : CS * SEG;
-            for (int b = 0; b < n; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
-        }
-    }
-}
-
 }  // namespace
-
-#ifndef SM_ADV_CS
-#define SM_ADV_CS 1      // consecutive 16-B segments per thread (1: ad_volume_kernel)
-#endif
-#ifndef SM_ADV_CS_ROWS
-#define SM_ADV_CS_ROWS 8
-#endif
 
 hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int64_t fstride, int batch,
                             int D, uint8_t* dif, int64_t dstride, hipStream_t s) {
     constexpr int SEG = 16;
     const int nseg = (W + SEG - 1) / SEG;
     if (W <= 0 || H <= 0 || D <= 0 || batch <= 0 || nseg > 4 * kVT) return hipErrorInvalidValue;
-    if constexpr (SM_ADV_CS > 1) {
-        const int ngrp = (nseg + SM_ADV_CS - 1) / SM_ADV_CS;
-        int rb = SM_ADV_CS_ROWS;
-        while (rb > 1 && rb * ngrp > kVT) --rb;
-        if (rb > H) rb = H;
-        if (rb * ngrp <= kVT) {
-            const size_t lds = (size_t)rb * ((SEG + ngrp * SM_ADV_CS * SEG + 4) / 4) * 4;
-            const int dsplit = std::max(1, std::min(D, SM_ADV_MAXSPLIT));
-            const dim3 grid((unsigned)((H + rb - 1) / rb), (unsigned)batch, (unsigned)dsplit);
-            hipLaunchKernelGGL(ad_volume_cs_kernel<SM_ADV_CS>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb,
-                               dsplit, dif, dstride);
-            return hipGetLastError();
-        }
-    }
     // rows per block: up to SM_ADV_ROWS, at most 4 segments per thread
     int rb = SM_ADV_ROWS;
     while (rb > 1 && rb * nseg > 4 * kVT) --rb;
@@ -346,25 +184,16 @@ hipError_t launch_ad_volume(const uint8_t* L, const uint8_t* R, int W, int H, in
     // 59.6; plain instead of nontemporal stores 49.2.  Round 4 (one box): 4 x 16 50.2; 4 x 8 50.7;
     // 2 x 4 50.7; 4 x 2 53.7; 2 x 2 52.1 (kept: the fewest re-reads of the band, see SM_ADV_MAXSPLIT)
     const int dsplit = std::max(1, std::min(D, SM_ADV_MAXSPLIT));
-    const int gc = dsplit % SM_ADV_GC == 0 ? SM_ADV_GC : 1;
-#if SM_ADV_ORDER == 3
-    const dim3 grid((unsigned)bands, (unsigned)dsplit, (unsigned)batch);
-#elif SM_ADV_ORDER
-    const int64_t nblk = (int64_t)bands * batch * dsplit;
-    if (nblk > 0x7FFFFFFF) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)nblk);
-#else
     const dim3 grid((unsigned)bands, (unsigned)batch, (unsigned)dsplit);
-#endif
     if (kf <= 1)
-        hipLaunchKernelGGL(ad_volume_kernel<1>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
-                           dif, dstride);
+        hipLaunchKernelGGL(ad_volume_kernel<1>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, dsplit, dif,
+                           dstride);
     else if (kf == 2)
-        hipLaunchKernelGGL(ad_volume_kernel<2>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
-                           dif, dstride);
+        hipLaunchKernelGGL(ad_volume_kernel<2>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, dsplit, dif,
+                           dstride);
     else
-        hipLaunchKernelGGL(ad_volume_kernel<4>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, bands, dsplit, gc,
-                           dif, dstride);
+        hipLaunchKernelGGL(ad_volume_kernel<4>, grid, dim3(kVT), lds, s, L, R, W, H, pitch, fstride, D, rb, dsplit, dif,
+                           dstride);
     return hipGetLastError();
 }
 
