@@ -204,3 +204,19 @@ def test_wide_path_slice_keys(matcher, oracle):
         torch.cuda.synchronize()
         assert np.array_equal(k.cpu().numpy().view(np.uint32), oracle.box_keys_slice(L, R, 21, a, b)), (a, b)
     assert np.array_equal(matcher.dslice_rehearse(L, R, 21, 64, 3), oracle.box_disp(L, R, 21, 64))
+
+
+def test_wide_path_frame_groups_partial_last_group(matcher, oracle):
+    """Frame groups of the wide path (bm_wide.hip: up to 4 frames per vsum/hwta pair, ceil(2048 / H) of
+    them): 5 frames of height 700 run as a group of 3 and a group of 2; every frame, left and right view,
+    equal to the oracle."""
+    import torch
+    pairs = [oracle.synth_pair(300 + i, 96, 700, 32) for i in range(5)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, 19, 24)
+    outlr = matcher.match_device(Lt, Rt, 19, 24, lr_check=True)
+    torch.cuda.synchronize()
+    for i, (L, R) in enumerate(pairs):
+        assert np.array_equal(out[i].cpu().numpy(), oracle.box_disp(L, R, 19, 24)), i
+        assert np.array_equal(outlr[i].cpu().numpy(), oracle.box_lr(L, R, 19, 24)[2]), i
