@@ -90,8 +90,11 @@ size_t wide_workspace_bytes(int W, int H, int D, int batch);
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s);
 constexpr int kMaxWideWidth = 4096;
-// radius 16..127 and 4 <= W <= 4096 take the separable wide-window path (bm_wide.hip); the rest the generic kernel
-inline bool wide_path(int radius, int W) { return radius > kMaxBoxRadius && W >= 4 && W <= kMaxWideWidth; }
+// radius 16..127, 4 <= W <= 4096 and frames below 2^31 bytes (its buffer loads address a frame with 32-bit
+// offsets) take the separable wide-window path (bm_wide.hip); the rest the generic kernel
+inline bool wide_path(int radius, int W, int H, int pitch) {
+    return radius > kMaxBoxRadius && W >= 4 && W <= kMaxWideWidth && (int64_t)pitch * H < ((int64_t)1 << 31);
+}
 // SM_DEVICE_CU_GRID (bm_literal.hip): Device.cu's literal map, AD only for rows < 256 and cols < 320, all zero
 // for W > 1024; needs W >= 320, H >= 256 and literal_workspace_bytes(D) of device scratch in `ws`
 size_t literal_workspace_bytes(int D);

@@ -349,7 +349,7 @@ size_t wide_workspace_bytes(int W, int H, int D, int batch) {
 
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
                                  int64_t rstride, hipStream_t s) {
-    if (a.W < 4 || a.H <= 0 || a.W > 4096 || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
+    if (!wide_path(kMaxBoxRadius + 1, a.W, a.H, a.pitch) || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
         return hipErrorInvalidValue;
     const int nd = a.d_hi - a.d_lo;
     const int G = wide_group(a.H, batch);

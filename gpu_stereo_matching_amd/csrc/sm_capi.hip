@@ -245,7 +245,7 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
     const bool guided_right = lr && guided;   // right view fused into the guided pass (bm_guided.hip)
     // box r > 15: the separable wide-window path (bm_wide.hip), right view included; wider frames keep the
     // direct generic kernel and the mirrored LR pass
-    const bool wide = !guided && sm::wide_path(radius, W);
+    const bool wide = !guided && sm::wide_path(radius, W, H, pitch);
     if ((flags & SM_DEVICE_CU_GRID) != 0) {   // Device.cu's launch geometry, frame by frame (bm_literal.hip)
         if (flags != SM_DEVICE_CU_GRID || lr)
             return fail(SM_ERR_INVALID_ARG, "SM_DEVICE_CU_GRID is box aggregation only (flags 0x%x)", flags);
@@ -772,7 +772,7 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
     a.thresh_key = seed_key(radius);
     a.keys = keys;
     if (!rkeys) {
-        if (sm::wide_path(radius, W)) {   // the wide-window path (bm_wide.hip)
+        if (sm::wide_path(radius, W, H, pitch)) {   // the wide-window path (bm_wide.hip)
             int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo, 1));
             if (rc) return rc;
             SM_HIP(sm::launch_box_match_wide(a, 1, reinterpret_cast<uint16_t*>(h->d_vol), nullptr, 0, 0, s));
@@ -1203,7 +1203,7 @@ SM_API int sm_slice_keys_device(sm_handle* h, const uint8_t* d_left, const uint8
     hipStream_t s = (hipStream_t)stream;
     // radius > 15 runs the wide-window path through the handle's volume workspace: ordered after the handle's
     // last workspace pass on another stream, as run_device orders its passes
-    const bool ws = sm::wide_path(radius, width);
+    const bool ws = sm::wide_path(radius, width, height, pitch);
     if (ws && h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
     rc = slice_keys_pass(h, d_left, d_right, width, height, pitch, radius, d_lo, d_hi, false, d_keys, nullptr, s);
     if (ws) {
