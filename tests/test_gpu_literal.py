@@ -220,3 +220,17 @@ def test_wide_path_frame_groups_partial_last_group(matcher, oracle):
     for i, (L, R) in enumerate(pairs):
         assert np.array_equal(out[i].cpu().numpy(), oracle.box_disp(L, R, 19, 24)), i
         assert np.array_equal(outlr[i].cpu().numpy(), oracle.box_lr(L, R, 19, 24)[2]), i
+
+
+@pytest.mark.parametrize("W,H", [(4, 1), (5, 3), (7, 40), (8, 2), (13, 17)])
+def test_wide_path_tiny_frames(matcher, oracle, W, H):
+    """The wide path's smallest frames (4 <= W < 16, a single row): clamped dword columns and the
+    per-lane byte shifts cover every column; left map and LR equal the oracle."""
+    rng = np.random.default_rng(W * 100 + H)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    for D in (1, 3, W + 2):
+        assert np.array_equal(matcher.match(L, R, 16, D), oracle.box_disp(L, R, 16, D)), D
+        chk, rd, mask = matcher.match_lr(L, R, 16, D)
+        _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, 16, D)
+        assert np.array_equal(rd, rd_o) and np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o), D
