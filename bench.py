@@ -389,6 +389,59 @@ def cpu_baseline_all_cores(W, H, D, r, seed):
             "sample": f"{n} frames {W}x{H} D={D} r={r}, one per process on {n} cores, {dt:.2f} s"}
 
 
+def run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, stream, backend, steps):
+    """N > 1 only: one frame split over the ranks, d-slices (cfg4, d_max 256, MIN reduction of the slice keys,
+    both collectives) and row bands (r-row halo, all-gather of uint8 bands); whole-job maps/s on the
+    max-over-ranks clock."""
+    from gpu_stereo_matching_amd import sharding
+    D4 = 256
+    keys, dflat = sharding.dslice_buffers(H, W, world, dev)
+    d1 = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    n = max(10, steps // 4)
+    dslice = {"config": f"cfg4: {W}x{H} d_max={D4} r={r}, one frame d-sharded over {world} ranks",
+              "unit": "disparity-maps/s", "scaling": "strong", "keys_bytes_per_frame": W * H * 4}
+    for coll, label in (("rs_ag", f"reduce_scatter MIN int32 + all_gather uint8 ({backend})"),
+                        ("allreduce", f"all_reduce MIN int32 ({backend})")):
+        def dstep():
+            sharding.match_dslice(m, Lt[0], Rt[0], r, D4, rank, world, keys_t=keys, out_t=dflat, stream=stream,
+                                  collective=coll)
+
+        for _ in range(5):
+            dstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(n):
+            dstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        dslice[coll] = {"value": round(n / float(dt.item()), 2), "ms_per_frame": round(float(dt.item()) * 1000 / n, 4),
+                        "collective": label}
+
+    # row bands of one frame (r-row halo, all-gather of uint8 bands)
+    def bstep():
+        sharding.match_rowband(m, Lt[0], Rt[0], r, D, rank, world, out_t=d1, stream=stream)
+
+    for _ in range(5):
+        bstep()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(n):
+        bstep()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    rowband = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
+               "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_gather uint8 bands ({backend})",
+               "halo_rows": r, "scaling": "strong"}
+
+    return dslice, rowband
+
+
 def main():
     args = parse()
     if args.profile:
@@ -482,51 +535,11 @@ def main():
     # ---- d-slice sharding of one frame (N > 1): cfg4, 1080p d_max=256, MIN reduction of the slice keys ----
     dslice = rowband = None
     if distributed:
-        from gpu_stereo_matching_amd import sharding
-        D4 = 256
-        keys, dflat = sharding.dslice_buffers(H, W, world, dev)
-        d1 = torch.empty((H, W), dtype=torch.uint8, device=dev)
-        n = max(10, args.steps // 4)
-        dslice = {"config": f"cfg4: {W}x{H} d_max={D4} r={r}, one frame d-sharded over {world} ranks",
-                  "unit": "disparity-maps/s", "scaling": "strong", "keys_bytes_per_frame": W * H * 4}
-        for coll, label in (("rs_ag", f"reduce_scatter MIN int32 + all_gather uint8 ({backend})"),
-                            ("allreduce", f"all_reduce MIN int32 ({backend})")):
-            def dstep():
-                sharding.match_dslice(m, Lt[0], Rt[0], r, D4, rank, world, keys_t=keys, out_t=dflat, stream=stream,
-                                      collective=coll)
-
-            for _ in range(5):
-                dstep()
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            t1 = time.perf_counter()
-            for _ in range(n):
-                dstep()
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            dslice[coll] = {"value": round(n / float(dt.item()), 2), "ms_per_frame": round(float(dt.item()) * 1000 / n, 4),
-                            "collective": label}
-
-        # row bands of one frame (r-row halo, all-gather of uint8 bands)
-        def bstep():
-            sharding.match_rowband(m, Lt[0], Rt[0], r, D, rank, world, out_t=d1, stream=stream)
-
-        for _ in range(5):
-            bstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t1 = time.perf_counter()
-        for _ in range(n):
-            bstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        rowband = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
-                   "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_gather uint8 bands ({backend})",
-                   "halo_rows": r, "scaling": "strong"}
+        try:
+            dslice, rowband = run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, stream,
+                                               backend, args.steps)
+        except Exception as e:  # report, never hide; the headline above is already measured
+            dslice = {"error": f"{type(e).__name__}: {e}"}
 
     # ---- cfg5 as BASELINE configs[4] writes it: 4K pairs, d_max=192, guided + LR, frames batched
     #      over every rank (frame-parallel, no collective), whole-job maps/s with the max-over-ranks clock ----
@@ -566,35 +579,38 @@ def main():
                     "ms_per_step": round(dt5 * 1000 / n5, 4), "steps": n5, "n_gpus": world, "scaling": "weak",
                     "kernel": "guided_fused_kernel<5, true>", "dtype": "fp32 (u8 in/out)"}
             if distributed:
-                # the north star's split on the configuration it pays for: ONE 4K guided + LR
-                # frame d-sharded over the ranks, left and right keys through two MIN reduce-scatters, the
-                # LR check on the gathered maps (sharding.match_dslice(lr_check=True))
-                from gpu_stereo_matching_amd import sharding
-                m5.set_guided_eps(1e-4 * 255 * 255)
-                kb5 = sharding.dslice_buffers(H5, W5, world, dev)
-                rb5 = sharding.dslice_buffers(H5, W5, world, dev)
+                try:
+                    # the north star's split on the configuration it pays for: ONE 4K guided + LR
+                    # frame d-sharded over the ranks, left and right keys through two MIN reduce-scatters, the
+                    # LR check on the gathered maps (sharding.match_dslice(lr_check=True))
+                    from gpu_stereo_matching_amd import sharding
+                    m5.set_guided_eps(1e-4 * 255 * 255)
+                    kb5 = sharding.dslice_buffers(H5, W5, world, dev)
+                    rb5 = sharding.dslice_buffers(H5, W5, world, dev)
 
-                def dstep5():
-                    sharding.match_dslice(m5, L5[0], R5[0], r, D5, rank, world, keys_t=kb5[0], out_t=kb5[1],
-                                          stream=stream, agg="guided", lr_check=True, right_bufs=rb5)
+                    def dstep5():
+                        sharding.match_dslice(m5, L5[0], R5[0], r, D5, rank, world, keys_t=kb5[0], out_t=kb5[1],
+                                              stream=stream, agg="guided", lr_check=True, right_bufs=rb5)
 
-                for _ in range(2):
-                    dstep5()
-                torch.cuda.synchronize(dev)
-                dist.barrier()
-                t1 = time.perf_counter()
-                for _ in range(n5):
-                    dstep5()
-                torch.cuda.synchronize(dev)
-                dist.barrier()
-                t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                cfg5["dslice_guided_lr"] = {
-                    "config": f"cfg5 one {W5}x{H5} frame, guided + LR, d_max={D5}, d-sharded over {world} ranks: "
-                              f"left + right slice keys, two MIN reduce_scatter int32 + two all_gather uint8 "
-                              f"({backend}), LR check", "value": round(n5 / float(t.item()), 2),
-                    "unit": "disparity-maps/s", "ms_per_frame": round(float(t.item()) * 1000 / n5, 4),
-                    "scaling": "strong", "keys_bytes_per_frame": W5 * H5 * 8}
+                    for _ in range(2):
+                        dstep5()
+                    torch.cuda.synchronize(dev)
+                    dist.barrier()
+                    t1 = time.perf_counter()
+                    for _ in range(n5):
+                        dstep5()
+                    torch.cuda.synchronize(dev)
+                    dist.barrier()
+                    t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    cfg5["dslice_guided_lr"] = {
+                        "config": f"cfg5 one {W5}x{H5} frame, guided + LR, d_max={D5}, d-sharded over {world} ranks: "
+                                  f"left + right slice keys, two MIN reduce_scatter int32 + two all_gather uint8 "
+                                  f"({backend}), LR check", "value": round(n5 / float(t.item()), 2),
+                        "unit": "disparity-maps/s", "ms_per_frame": round(float(t.item()) * 1000 / n5, 4),
+                        "scaling": "strong", "keys_bytes_per_frame": W5 * H5 * 8}
+                except Exception as e:  # report, never hide
+                    cfg5["dslice_guided_lr"] = {"error": f"{type(e).__name__}: {e}"}
         finally:
             m5.close()
 
