@@ -5,20 +5,22 @@
 //   wide_vsum_kernel : V_d(y, c) = sum of AD_d over rows y-r..y+r (clipped), AD_d(y, c) = |L(y,c) - R(y,c-d)|
 //                      for c >= d else 0 (Device.cu:27-31); one lane per 4 columns walks a chunk of rows with
 //                      packed-u16 running sums (V <= 255 * 255 = 65025), 8 rows' dword loads in flight at a
-//                      time, one d per block row; u16 planes written 8 B per lane per row.
+//                      time (buffer loads, row offset in the SGPR soffset), one d per block row; u16 planes
+//                      written nontemporally, 8 B per lane per row.
 //   wide_hwta_kernel : one 256-lane block per image row: per d the row of V (prefetched one d ahead) is
 //                      prefix-summed across the block (local prefix + DPP wave scan + 4-wave offsets) into LDS,
 //                      each output's window sum is two prefix reads, and the key (S << 8 | d) is min-folded in
 //                      registers with the validity d <= W - x (Device.cu:44) and the 50 win^2 seed (:37).  The
 //                      right view's candidate for u = x - d (C_R(u, d) = C_L(u + d, d), StereoHelper.cpp:
 //                      156-180) is folded into an LDS row by atomic min, so LR needs no second pass.
-// HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R come from L2.
+// Frames go through in groups of up to 4 per vsum / hwta pair (wide_group: ~8 row blocks per CU), V planes of
+// the group in the handle's workspace.  HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R
+// come from L2.
 // Exact integer arithmetic throughout: S <= 255 * 255^2 < 2^24, prefix sums < 4096 * 65025 < 2^32.
 #include <algorithm>
 #include <type_traits>
 
 #include "bm_common.h"
-
 
 namespace sm {
 namespace {
