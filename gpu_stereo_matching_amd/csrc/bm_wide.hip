@@ -13,8 +13,8 @@
 //                      registers with the validity d <= W - x (Device.cu:44) and the 50 win^2 seed (:37).  The
 //                      right view's candidate for u = x - d (C_R(u, d) = C_L(u + d, d), StereoHelper.cpp:
 //                      156-180) is folded into an LDS row by atomic min, so LR needs no second pass.
-// Frames go through in groups of up to 4 per vsum / hwta pair (wide_group: ~8 row blocks per CU), V planes of
-// the group in the handle's workspace.  HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R
+// Frames go through in groups of up to 8 per vsum / hwta pair (wide_group: ~32 row blocks per CU, at most
+// 4.5 GB of V planes), the group's planes in the handle's workspace.  HBM per (pixel, d): 2 B written + 2 B read (the V planes); L and R
 // come from L2.
 // Exact integer arithmetic throughout: S <= 255 * 255^2 < 2^24, prefix sums < 4096 * 65025 < 2^32.
 #include <algorithm>
@@ -336,17 +336,21 @@ hipError_t launch_span(const uint16_t* V, int W, int H, int radius, int d_lo, in
     return launch_h<NPT, 256>(V, W, H, radius, d_lo, d_hi, seed, thresh, out, frames, s);
 }
 
-// frames per vsum / hwta launch pair: enough row blocks for ~8 per CU (1080 rows of one 1080p frame give 4);
-// 1080p: 2 frames per pair measured 7-8 % faster than 1, 4 the same as 2
-int wide_group(int H, int batch) {
-    const int want = (2048 + H - 1) / H;
-    return std::max(1, std::min({want, batch, 4}));
+// frames per vsum / hwta launch pair: enough row blocks for ~32 per CU (1080 rows of one 1080p frame give 4),
+// at most 8 frames and 4.5 GB of V planes (1080p D=128: 8 frames, 4.2 GB).  Same box, 1080p D=128, 8 frames per
+// call (profiles/microbench/r05_wide_path.txt): 2 / 4 / 8 frames per pair 0.280 / 0.268 / 0.265 ms at r = 16,
+// 0.280 / 0.251 / 0.239 at r = 127
+int wide_group(int W, int H, int D, int batch) {
+    const int64_t plane = (int64_t)W * H * D * (int64_t)sizeof(uint16_t);
+    const int by_mem = (int)std::max<int64_t>(1, ((int64_t)4608 << 20) / std::max<int64_t>(plane, 1));
+    const int want = (8192 + H - 1) / H;
+    return std::max(1, std::min({want, batch, 8, by_mem}));
 }
 
 }  // namespace
 
 size_t wide_workspace_bytes(int W, int H, int D, int batch) {
-    return (size_t)wide_group(H, batch) * D * W * H * sizeof(uint16_t);
+    return (size_t)wide_group(W, H, D, batch) * D * W * H * sizeof(uint16_t);
 }
 
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
@@ -354,7 +358,7 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
     if (!wide_path(kMaxBoxRadius + 1, a.W, a.H, a.pitch) || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
         return hipErrorInvalidValue;
     const int nd = a.d_hi - a.d_lo;
-    const int G = wide_group(a.H, batch);
+    const int G = wide_group(a.W, a.H, nd, batch);
     // row chunks: enough waves to fill the chip (~32 per CU), each chunk at least a window tall (its prologue
     // re-reads the 2r + 1 rows above it, from L2)
     const unsigned gx = (unsigned)((a.W + 4 * kVT - 1) / (4 * kVT));
