@@ -34,9 +34,6 @@ constexpr int kSO = kSC - 16;      // K2: output columns per strip (the strip st
 #ifndef SM_SAD_BLOCKS
 #define SM_SAD_BLOCKS 16384
 #endif
-#ifndef SM_SAD_PF
-#define SM_SAD_PF 1   // next row group in flight: 154.6 vs 156.8 us per frame (same box, 5 rounds)
-#endif
 constexpr int kSadBlocks = SM_SAD_BLOCKS;  // K2 blocks per launch (>= 32-row bands)
 // K2 walking direction (round 4): odd bands walk their rows bottom-up, so the 2r halo
 // rows two neighbouring bands share are read by both at the same phase of their walks (both at the
@@ -193,8 +190,8 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
             flush(yi - R);
         }
     };
-#if SM_SAD_PF
-    // two row groups in flight: group g + 1 loads while group g runs (A / B buffers, no copies)
+    // two row groups in flight: group g + 1 loads while group g runs (A / B buffers, no copies; one group at a
+    // time measured 156.8 against 154.6 us per frame, same box, 5 rounds)
     Words<NG> na[K], nb[K];
     load_group(yo0 - R, na);
     for (int base = yo0 - R; base < yi_end; base += 2 * K) {
@@ -204,13 +201,6 @@ __global__ __launch_bounds__(kST) void box_sad_kernel(const uint8_t* __restrict_
         load_group(base + 2 * K, na);
         run_group(base + K, nb);
     }
-#else
-    for (int base = yo0 - R; base < yi_end; base += K) {
-        Words<NG> nw[K];
-        load_group(base, nw);
-        run_group(base, nw);
-    }
-#endif
 }
 
 // K3: 8 pixels per thread, one 16-B nontemporal load per d plane (the volume is streamed once and
