@@ -81,6 +81,20 @@ def test_single_frame_cpp(tmp_path, gray, bm_expected, pair, sad, rng):
 
 
 @pytest.mark.gpu
+def test_single_frame_cpp_wide_window(tmp_path, gray, oracle):
+    """An unchanged singleFrame() caller with SADWindowSize 20 (41 x 41, Device.cu's unbounded window):
+    blockMatching_gpu runs the separable wide-window path (bm_wide.hip) and writes the oracle's map."""
+    L, R = gray["Art/view1"], gray["Art/view5"]
+    _write_pgm(tmp_path / "l.pgm", L)
+    _write_pgm(tmp_path / "r.pgm", R)
+    env = dict(os.environ, SM_LEFT=str(tmp_path / "l.pgm"), SM_RIGHT=str(tmp_path / "r.pgm"),
+               SM_OUT=str(tmp_path / "d.pgm"), SM_SAD="20", SM_RANGE="64", SM_QUIET="1")
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_read_pgm(tmp_path / "d.pgm"), oracle.box_disp(L, R, 20, 64))
+
+
+@pytest.mark.gpu
 def test_single_frame_cpp_device_group(tmp_path, gray, bm_expected):
     """SM_DEVICES=0,0,0: the unchanged singleFrame() caller runs through a 3-member group handle
     (row bands, one per member) and still writes the golden map."""
