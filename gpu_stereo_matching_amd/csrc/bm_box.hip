@@ -43,6 +43,9 @@ template <bool RIGHT, int R, int DMAX>
 constexpr int kWavesD = (kWideRight<RIGHT, R> && DMAX == 192) ? 6 : kWaves<RIGHT, R>;
 // right-view scatter: pair the two candidates of one u in registers (one ds_min per u) except where
 // the extra live values push the fused loop past 128 VGPRs (r = 3: NQ = 16)
+// (round 5, same box: unpaired, two ds_min_u32 per output and pair, ran box + LR 86.1 against 79.2 us per
+// 1080p frame and 591 against 551 at 4K D=192: the scatter is LDS-atomic-bound; profiles/microbench/
+// r05_box_lr_paired_scatter_ab.txt)
 template <int R>
 constexpr bool kPairedScatter = (R != 3);
 // radius 8..15 (WIDE): the packed u16 column sums still fit (<= (32 + 2r) * 255), the window sums do
