@@ -27,6 +27,7 @@ namespace {
 
 using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -101,7 +102,7 @@ __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const u
         }
     }
     const bool full = c4 + 4 <= W;
-    constexpr int kU = 8;
+    constexpr int kU = 8;   // 4 and 16 measured the same (profiles/microbench/r05_wide_path.txt)
     // one batch of kU rows: the kU entering and kU leaving rows, clamped into the frame, loaded together
     // (4 kU loads in flight), then the sums; EDGE batches (a row entering past H or leaving above 0,
     // wave-uniform) mask those rows' AD
@@ -123,8 +124,8 @@ __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const u
                 if (full) {
                     // nontemporal: the planes are streamed once each way (plain stores and loads measured
                     // 8-13 % slower over both kernels)
-                    __builtin_nontemporal_store(v01, reinterpret_cast<uint32_t*>(dst));
-                    __builtin_nontemporal_store(v23, reinterpret_cast<uint32_t*>(dst) + 1);
+                    const u32x2 v = {v01, v23};
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(dst));
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
