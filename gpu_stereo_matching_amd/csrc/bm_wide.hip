@@ -171,11 +171,6 @@ __global__ __launch_bounds__(kVT) void wide_vsum_kernel(const uint8_t* __restric
     vsum_walk(L, R, W, H, pitch, radius, d, c4, y0, y1, Vd);
 }
 
-// NPT outputs per thread (W <= 256 * NPT), contiguous: x in [8t, 8t + 8) for NPT 8.  The prefix row lives in LDS
-// with one pad dword after every 8 (index i -> i + i / 8), so the 64 lanes' segment stores and their window
-// reads (lanes 9 dwords apart) fall on distinct banks.  Dynamic LDS: pref[2][NPAD] u32 (double-buffered over
-// d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.  (Two d per
-// barrier pair, DP = 2, measured 7-20 % slower: profiles/microbench/r05_wide_path.txt.)
 struct WideOut {
     uint8_t* disp;    // left map (or null), out_pitch / out_frame_stride
     int opitch;
@@ -186,7 +181,12 @@ struct WideOut {
     int64_t rfs;
 };
 
-// grid (H, frames of the group)
+// One block per image row, grid (H, frames of the group).
+// NPT outputs per thread (W <= 256 * NPT), contiguous: x in [8t, 8t + 8) for NPT 8.  The prefix row lives in LDS
+// with one pad dword after every 8 (index i -> i + i / 8), so the 64 lanes' segment stores and their window
+// reads (lanes 9 dwords apart) fall on distinct banks.  Dynamic LDS: pref[2][NPAD] u32 (double-buffered over
+// d: two barriers per d), then rmin[NPAD] u32 (same padding) when the right view is requested.  (Two d per
+// barrier pair, DP = 2, measured 7-20 % slower: profiles/microbench/r05_wide_path.txt.)
 template <int NPT, int NT>
 __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restrict__ V, int W, int H, int radius,
                                                         int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
@@ -365,8 +365,13 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
     const unsigned gx = (unsigned)((a.W + 4 * kVT - 1) / (4 * kVT));
     const int64_t waves = (int64_t)gx * nd * G;
     const int want = (int)std::max<int64_t>(1, (8192 + waves - 1) / waves);
-    const int chunk = std::max({(a.H + want - 1) / want, 2 * a.radius + 1, 32});
-    const int nch = (a.H + chunk - 1) / chunk;
+    int chunk = std::max({(a.H + want - 1) / want, 2 * a.radius + 1, 32});
+    int nch = (a.H + chunk - 1) / chunk;
+    if ((int64_t)nch * G > 65535) {   // grid.z limit (very tall frames): longer chunks
+        const int nmax = 65535 / G;
+        chunk = (a.H + nmax - 1) / nmax;
+        nch = (a.H + chunk - 1) / chunk;
+    }
     for (int f = 0; f < batch; f += G) {
         const int n = std::min(G, batch - f);
         hipLaunchKernelGGL(wide_vsum_kernel, dim3(gx, (unsigned)nd, (unsigned)(nch * n)), dim3(kVT), 0, s,
