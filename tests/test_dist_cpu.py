@@ -236,3 +236,10 @@ def test_box_keys_above_2_31_reduce_unsigned_gloo(tmp_path):
     for k in range(2):
         for coll in ("allreduce", "rs_ag"):
             assert (np.load(tmp_path / f"bias{k}_{coll}.npy") == 5).all(), (k, coll)
+
+
+def test_box_keys_fit_signed_int32_at_every_radius():
+    """The torch d-slice collectives take a signed int32 MIN of the box keys: every key is min'ed with the
+    seed (50 win^2) << 8 (Device.cu:37), which stays below 2^31 up to the largest radius (127)."""
+    assert all(sharding.seed_key(r) < (1 << 31) for r in range(128))
+    assert sharding.seed_key(127) == (50 * 255 * 255) << 8

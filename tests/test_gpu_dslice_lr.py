@@ -146,17 +146,17 @@ def test_dslice_lr_rejects_wide_box_radius(single):
 
 @pytest.mark.parametrize("coll", ["rs_ag", "allreduce"])
 def test_dslice_torch_wide_radius_keys_above_2_31(coll):
-    """sharding.match_dslice at r = 100 through torch.distributed / RCCL (world 1): on 0/255 frames the
-    box keys pass 2^31 and travel biased (sharding.box_keys_biased) through the signed MIN; the map equals
-    the single pass's."""
+    """sharding.match_dslice at r = 100 through torch.distributed / RCCL (world 1): the box keys pass 2^31
+    and travel biased (sharding.box_keys_biased) through the collectives; the map equals the single pass's.
+    (The multi-rank ordering itself is tests/test_dist_cpu.py::test_box_keys_above_2_31_reduce_unsigned_gloo.)"""
     import torch
     import torch.distributed as dist
     import gpu_stereo_matching_amd as sm
     from gpu_stereo_matching_amd import sharding
-    rng = np.random.default_rng(100)
-    H, W, D, r = 210, 300, 12, 100
-    L = (rng.integers(0, 2, (H, W)) * 255).astype(np.uint8)
-    R = np.where(np.arange(W)[None, :] < W // 2, L, 255 - L).astype(np.uint8)
+    H, W, D, r = 210, 400, 12, 100
+    L = np.full((H, W), 255, np.uint8)   # AD 255 wherever x >= d: window sums up to 255 * 201^2 > 2^23
+    R = np.zeros((H, W), np.uint8)
+    R[:, :40] = 255                      # and a strip where the AD is small
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda:0"))
     try:
         with sm.BlockMatcher(0, 512, 256, 256) as m:
