@@ -77,20 +77,10 @@ def _host_staged(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-INT32_SIGN = -(1 << 31)   # XOR with this maps the unsigned order of u32 keys onto the signed order of int32
-
-
-def box_keys_biased(radius: int) -> bool:
-    """Box keys (SAD << 8 | d, unsigned) reach 2^31 once 255 * (2r + 1)^2 >= 2^23, i.e. r >= 91; the torch
-    collectives' MIN is a signed int32 MIN, so such keys travel XOR 2^31 (signed order = unsigned order)
-    and are XOR-ed back after the reduction.  Below r = 91 the keys stay as they are (no extra passes)."""
-    win = 2 * radius + 1
-    return 255 * win * win >= (1 << 23)
-
-
 def reduce_slice_keys(keys, group=None):
-    """In-place signed MIN all-reduce of an int32 key map (box keys below 2^31, or biased by
-    box_keys_biased; guided keys carry a signed cost)."""
+    """In-place signed MIN all-reduce of an int32 key map (box keys are < 2^31 by construction: every
+    key is min'ed with the seed (50 win^2) << 8, at most 832,320,000 at r = 127; guided keys carry a
+    signed cost)."""
     import torch.distributed as dist
     if keys.is_cuda and _host_staged(group):
         h = keys.cpu()
@@ -213,18 +203,11 @@ def match_dslice(matcher, left_t, right_t, radius: int, num_disp: int, rank: int
     keys_t[P:].fill_(fill)
     if stream is not None:
         torch.cuda.current_stream(left_t.device).wait_stream(stream)
-    bias = agg == "box" and box_keys_biased(radius)
-    if bias:
-        keys_t.bitwise_xor_(INT32_SIGN)
     if collective == "allreduce":
         reduce_slice_keys(keys_t, group)
-        if bias:
-            keys_t.bitwise_xor_(INT32_SIGN)
         to_disp(keys_t.view(1, -1), out_t.view(1, -1))
         return out_t[:P].view(H, W)
     chunk = reduce_scatter_keys(keys_t, world, group)
-    if bias:
-        chunk.bitwise_xor_(INT32_SIGN)
     n = chunk.numel()
     mine = to_disp(chunk.view(1, n))
     gather_disparity(mine.view(n), out_t, group)
@@ -319,17 +302,10 @@ def match_dslice_host_keys(keys, radius: int, world: int, collective: str = "rs_
         finish = lambda k: keys_to_disparity_host(k.view(np.uint32), radius)   # noqa: E731
     flat = torch.full((padded_pixels(H, W, world),), fill, dtype=torch.int32)
     flat[:P] = torch.from_numpy(np.ascontiguousarray(keys, np.int32).reshape(P))
-    bias = agg == "box" and box_keys_biased(radius)
-    if bias:
-        flat.bitwise_xor_(INT32_SIGN)
     if collective == "allreduce":
         reduce_slice_keys(flat, group)
-        if bias:
-            flat.bitwise_xor_(INT32_SIGN)
         return finish(flat.numpy()[:P]).reshape(H, W)
     chunk = reduce_scatter_keys(flat, world, group)
-    if bias:
-        chunk.bitwise_xor_(INT32_SIGN)
     mine = torch.from_numpy(finish(chunk.numpy()))
     out = torch.empty(flat.numel(), dtype=torch.uint8)
     gather_disparity(mine, out, group)

@@ -210,34 +210,6 @@ def test_rowband_allgather_gloo(tmp_path, world, H, mode):
             assert np.array_equal(got, want)
 
 
-def _bias_worker(rank, world, port, result_dir):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    # r = 100: box keys reach 2^31 (255 * 201^2 << 8 > 2^31).  Rank 0's slice holds keys above 2^31 (a SAD
-    # far above the threshold), rank 1's a key whose SAD is below it (d = 5): the unsigned minimum is
-    # rank 1's, which a plain signed int32 MIN would lose to rank 0's "negative" keys.
-    H, W = 3, 10
-    big = np.full((H, W), 0x90000000 | 1, np.uint32)
-    small = np.full((H, W), (0x100000 << 8) | 5, np.uint32)
-    keys = (big if rank == 0 else small).view(np.int32)
-    for coll in ("allreduce", "rs_ag"):
-        disp = sharding.match_dslice_host_keys(keys, 100, world, collective=coll)
-        np.save(os.path.join(result_dir, f"bias{rank}_{coll}.npy"), disp)
-    dist.destroy_process_group()
-
-
-def test_box_keys_above_2_31_reduce_unsigned_gloo(tmp_path):
-    """Box keys at radius >= 91 exceed 2^31: the signed int32 MIN of the torch collectives must still take
-    the unsigned minimum (sharding.box_keys_biased: keys travel XOR 2^31)."""
-    assert sharding.box_keys_biased(100) and not sharding.box_keys_biased(90)
-    port = _free_port()
-    mp.spawn(_bias_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    for k in range(2):
-        for coll in ("allreduce", "rs_ag"):
-            assert (np.load(tmp_path / f"bias{k}_{coll}.npy") == 5).all(), (k, coll)
-
-
 def test_box_keys_fit_signed_int32_at_every_radius():
     """The torch d-slice collectives take a signed int32 MIN of the box keys: every key is min'ed with the
     seed (50 win^2) << 8 (Device.cu:37), which stays below 2^31 up to the largest radius (127)."""

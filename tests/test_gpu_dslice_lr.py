@@ -142,30 +142,3 @@ def test_dslice_lr_rejects_wide_box_radius(single):
     L, R = _pair(80, 40, 16)
     with pytest.raises(sm.SMError):
         single.dslice_rehearse(L, R, 16, 16, 2, lr_check=True)
-
-
-@pytest.mark.parametrize("coll", ["rs_ag", "allreduce"])
-def test_dslice_torch_wide_radius_keys_above_2_31(coll):
-    """sharding.match_dslice at r = 100 through torch.distributed / RCCL (world 1): the box keys pass 2^31
-    and travel biased (sharding.box_keys_biased) through the collectives; the map equals the single pass's.
-    (The multi-rank ordering itself is tests/test_dist_cpu.py::test_box_keys_above_2_31_reduce_unsigned_gloo.)"""
-    import torch
-    import torch.distributed as dist
-    import gpu_stereo_matching_amd as sm
-    from gpu_stereo_matching_amd import sharding
-    H, W, D, r = 210, 400, 12, 100
-    L = np.full((H, W), 255, np.uint8)   # AD 255 wherever x >= d: window sums up to 255 * 201^2 > 2^23
-    R = np.zeros((H, W), np.uint8)
-    R[:, :40] = 255                      # and a strip where the AD is small
-    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda:0"))
-    try:
-        with sm.BlockMatcher(0, 512, 256, 256) as m:
-            Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
-            keys = m.slice_keys_device(Lt, Rt, r, 0, D)
-            got = sharding.match_dslice(m, Lt, Rt, r, D, 0, 1, collective=coll)
-            want = m.match_device(Lt, Rt, r, D)
-            torch.cuda.synchronize()
-            assert int((keys.view(torch.int32) < 0).sum()) > 0   # some keys above 2^31
-            assert np.array_equal(got.cpu().numpy(), want.cpu().numpy())
-    finally:
-        dist.destroy_process_group()
