@@ -18,9 +18,7 @@ if [ -n "$SM_VARIANT_ONLY" ]; then
 fi
 pids=()
 for f in $ALL; do
-  PF=""   # the product Makefile's per-file flags (FLAGS_bm_box)
-  [ "$f" = bm_box ] && PF="-mllvm -amdgpu-sched-strategy=iterative-maxocc"
-  /opt/rocm/bin/hipcc $FLAGS $PF -c $SRC/$f.hip -o $OUT/$f.o &
+  /opt/rocm/bin/hipcc $FLAGS -c $SRC/$f.hip -o $OUT/$f.o &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
