@@ -35,6 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# the fill ceiling measured on this part: torch's fill_ over 2.16 GB, one 16-B store per thread
+# (profiles/microbench/r05_write_ceiling.txt): the best write stream seen, the reference for write-bound kernels
+HBM_FILL_CEILING_GBS = 6850.0
 # VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction issues over 2 cycles per SIMD (32 lanes
 # per cycle, MI355X_MICROARCH.md "Execution model"), 2.4 GHz engine clock: 78.64 T lane-ops/s.  Measured
 # on this part (profiles/microbench/r02_valu_issue_*.txt): add/sub/mul/fma/shift 2.4 cycles per
@@ -81,14 +84,33 @@ def load_counts(path):
         return {}
 
 
-def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None):
+def code_hash(symbol):
+    """sha256 of the kernel's gfx950 machine code in the library this process loads (tools/codeobj.py)."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import codeobj
+        from gpu_stereo_matching_amd import _capi
+        return codeobj.kernel_sha256(_capi.LIB_PATH, symbol)
+    except Exception as e:  # report, never hide
+        return f"unavailable: {type(e).__name__}: {e}"
+
+
+def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None, symbol=None):
     """roofline on the binding resource of a compute-bound kernel: VALU lane-ops per second, from
     SQ_INSTS_VALU per launch (profiles/valu_counts.json, tools/valu_counts.py, same workload) over
-    the live launch time; LDS-array busy fraction from SQ_LDS_IDX_ACTIVE beside it."""
+    the live launch time; LDS-array busy fraction from SQ_LDS_IDX_ACTIVE beside it.  The counts are
+    used only when their entry's code_sha256 is the hash of the machine code this process runs
+    (VERDICT r5 item 3): after a kernel edit without a re-count, frac is null."""
     c = counts.get(key)
     if not c or c.get("workload") != list(workload):
         return {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TLANEOPS, 2), "unit": "T lane-op/s",
                 "frac": None, "kernel": kernel, "note": f"no SQ_INSTS_VALU count for {key} in profiles/valu_counts.json"}
+    live = code_hash(symbol or c.get("code_symbol", ""))
+    if c.get("code_sha256") != live:
+        return {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TLANEOPS, 2), "unit": "T lane-op/s",
+                "frac": None, "kernel": kernel, "code_sha256": live, "counts_code_sha256": c.get("code_sha256"),
+                "note": f"stale counts: profiles/valu_counts.json[{key}] was measured on other machine code than "
+                        "the library loaded here; re-run tools/valu_counts.py"}
     pl = c["per_launch"]
     t = launch_ms * 1e-3
     achieved = pl["SQ_INSTS_VALU"] * 64 / t / 1e12
@@ -97,7 +119,8 @@ def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None):
            "kernel_ms_per_launch": round(launch_ms, 5), "valu_wave_insts_per_launch": pl["SQ_INSTS_VALU"],
            "lds_busy_frac": round(pl["SQ_LDS_IDX_ACTIVE"] / (256 * t * CU_CLOCK_HZ), 4)
            if "SQ_LDS_IDX_ACTIVE" in pl else None,
-           "counts_source": "profiles/valu_counts.json (rocprofv3 --pmc SQ_INSTS_VALU, tools/valu_counts.py)"}
+           "counts_source": "profiles/valu_counts.json (rocprofv3 --pmc SQ_INSTS_VALU, tools/valu_counts.py)",
+           "code_sha256": live}
     # issue-cycle-weighted VALU busy: each wave64 VALU instruction costs the SIMD the cycles
     # measured for its encoding on this part (profiles/microbench/r02_valu_issue_cycles_pmc.txt: 2.37 for 32-bit
     # VOP1/VOP2, 4.25 for VOP3 such as v_perm_b32 / v_sad_u8 / v_min3_u32, 3.9 for conversions), averaged over
@@ -109,7 +132,10 @@ def valu_roofline(counts, key, workload, launch_ms, kernel, extra=None):
             mix = json.load(f)
     except (OSError, ValueError):
         mix = None
-    if mix and key.startswith("box_r5"):
+    if mix and key.startswith("box_r5") and mix.get("code_sha256") != live:
+        res["valu_issue_busy"] = None
+        res["valu_issue_note"] = "stale ISA mix: profiles/isa_mix_box.json describes other machine code"
+    elif mix and key.startswith("box_r5"):
         cyc = pl["SQ_INSTS_VALU"] * mix["avg_cycles_per_valu"]
         res["valu_issue_busy"] = round(cyc / (1024 * t * CU_CLOCK_HZ), 4)
         res["valu_avg_cycles_per_inst"] = mix["avg_cycles_per_valu"]
@@ -143,9 +169,9 @@ def cpu_baseline(W, H, D, r, seed):
                       f"{dt:.2f} s/map"}
 
 
-# BASELINE.json configs measured next to the headline (rank 0, device-resident synthetic pairs,
-# `batch` frames per call).  cfg1/cfg2 are quoted on the bundled Middlebury pairs; the bench uses
-# synthetic pairs of the same size because /root/reference is not on the GPU box.
+# BASELINE.json configs measured next to the headline (rank 0, device-resident pairs, `batch` frames per
+# call).  cfg1/cfg2 run on the reference's bundled Middlebury pairs (their gray fixtures, committed under
+# tests/golden); every other line uses synthetic pairs of the named size.
 VARIANTS = (
     # name, W, H, D, r, agg, lr, median, batch
     # cfg1 / cfg2 on the reference's own bundled Middlebury pairs (Art, Books, Dolls; gray fixtures
@@ -261,7 +287,14 @@ def run_variants(sm, torch, dev, stream, seed):
                                ("volume_wta_kernel", float(kt[2]), 2 * P * D + P)):
             g_ = nb / (kms * 1e-3) / 1e9
             per[kname] = {"ms": round(kms, 4), "algorithmic_bytes": nb, "achieved_GBs": round(g_, 1),
-                          "frac_of_hbm_peak": round(g_ / HBM_PEAK_GBS, 3), "frames_per_launch": SB}
+                          "frac_of_hbm_peak": round(g_ / HBM_PEAK_GBS, 3),
+                          "frac_of_fill_ceiling": round(g_ / HBM_FILL_CEILING_GBS, 3), "frames_per_launch": SB}
+        per["note"] = ("ms: HIP events around each kernel's launch on the product stream (median of 10 calls), so the "
+                       "dispatch gap is inside it; rocprofv3's kernel durations (profiles/*staged_roofline*.json) time "
+                       "the kernel alone and read 2-4 % higher fractions. The kernel's own roofline figure is the "
+                       "rocprof one; these live figures bound it from below. frac_of_fill_ceiling: against "
+                       f"{HBM_FILL_CEILING_GBS:.0f} GB/s, the fill rate measured on this part "
+                       "(profiles/microbench/r05_write_ceiling.txt)")
         out["staged kernels 1080p d128 (HBM roofline per kernel)"] = per
         # host frame stream, PCIe-inclusive: FrameStream overlaps H2D / match / D2H on three streams;
         # frames are produced in place in the pinned slots (next_inputs) and consumed in place
@@ -389,10 +422,93 @@ def cpu_baseline_all_cores(W, H, D, r, seed):
             "sample": f"{n} frames {W}x{H} D={D} r={r}, one per process on {n} cores, {dt:.2f} s"}
 
 
-def run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, stream, backend, steps):
+def rank_inventory(torch, dist, dev, backend):
+    """Every rank's device and PCI bus id (the first SCALE run records which GPUs it ran on)."""
+    p = torch.cuda.get_device_properties(dev)
+    bus = (getattr(p, "pci_domain_id", None), getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", None))
+    mine = {"rank": dist.get_rank(), "device": dev.index, "name": p.name,
+            "pci": "%04x:%02x:%02x" % bus if None not in bus else None}
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    return {"backend": backend, "world": dist.get_world_size(), "ranks": allr}
+
+
+def split_parity_box(sm, torch, dist, m, Lc, Rc, r, D4, rank, world, dev, stream):
+    """Before any split is timed: one cfg4 frame d-sharded over the ranks, both collectives,
+    against rank 0's single-GPU pass of the same frame, bit for bit on every rank (rank 0's map is broadcast and
+    each rank compares its gathered copy; the mismatch count is MAX-reduced)."""
+    from gpu_stereo_matching_amd import sharding
+    H, W = Lc.shape
+    ref = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    if rank == 0:
+        m.match_device(Lc, Rc, r, D4, out_t=ref, stream=stream)
+        torch.cuda.synchronize(dev)
+    dist.broadcast(ref, 0)
+    res = {}
+    for coll in ("rs_ag", "allreduce"):
+        got = sharding.match_dslice(m, Lc, Rc, r, D4, rank, world, stream=stream, collective=coll)
+        torch.cuda.synchronize(dev)
+        bad = torch.tensor([float((got != ref).sum().item())], dtype=torch.float64, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        res[coll] = int(bad.item())
+    return {"parity": all(v == 0 for v in res.values()), "rule": "bit-exact vs rank 0's single-GPU map, every rank",
+            "mismatching_pixels_max_over_ranks": res}
+
+
+def split_parity_guided_lr(sm, torch, dist, m5, L, R, r, D5, rank, world, dev, stream):
+    """One cfg5 guided + LR frame d-sharded over the ranks (MIN all-reduce of the left and right slice keys, so
+    every rank holds the reduced keys), against rank 0's single-member pass over [0, D5) of the same frame.
+    Tie-aware equality: every pixel's reduced key has the single pass's cost field (the keys quantise q to 2^-14,
+    and a slice's MIN picks the smallest quantised cost, so the cost fields must agree exactly); the d fields may
+    differ only where two disparities tie on that cost; and every pixel where the checked maps differ has such a
+    tie at its left pixel or at the right pixel either map points it to."""
+    from gpu_stereo_matching_amd import sharding
+    H, W = L.shape
+    P = H * W
+    kb = sharding.dslice_buffers(H, W, world, dev)
+    rb = sharding.dslice_buffers(H, W, world, dev)
+    chk = sharding.match_dslice(m5, L, R, r, D5, rank, world, keys_t=kb[0], out_t=kb[1], stream=stream,
+                                agg="guided", lr_check=True, right_bufs=rb, collective="allreduce")
+    torch.cuda.synchronize(dev)
+    if rank != 0:
+        dist.barrier()
+        return None
+    lk_ds, rk_ds = kb[0][:P].view(H, W).clone(), rb[0][:P].view(H, W).clone()
+    chk_ds = chk.clone()
+    lk, rk = m5.slice_keys_lr_device(L, R, r, 0, D5, agg="guided", stream=stream)
+    left = m5.guided_keys_to_disp_device(lk)
+    right = m5.right_keys_to_disp_device(rk)
+    chk_1 = m5.lr_check_device(left, right)
+    left_ds = m5.guided_keys_to_disp_device(lk_ds)
+    fused = m5.match_device(L, R, r, D5, agg="guided", lr_check=True, stream=stream)
+    torch.cuda.synchronize(dev)
+    cost_l = bool(torch.equal(lk_ds >> 8, lk >> 8))
+    cost_r = bool(torch.equal(rk_ds >> 8, rk >> 8))
+    tie_l, tie_r = lk_ds != lk, rk_ds != rk
+    xs = torch.arange(W, device=dev).view(1, W).expand(H, W)
+
+    def right_tie_at(d):
+        u = xs - d.long()
+        return tie_r.gather(1, u.clamp(min=0)) & (u >= 0)
+
+    mism = chk_ds != chk_1
+    just = tie_l | right_tie_at(left_ds) | right_tie_at(left)
+    unjust = int((mism & ~just).sum().item())
+    dist.barrier()
+    return {"parity": cost_l and cost_r and unjust == 0,
+            "rule": "tie-aware: reduced key cost fields == single pass's (left and right), checked-map differences "
+                    "only at cost ties",
+            "left_cost_fields_equal": cost_l, "right_cost_fields_equal": cost_r,
+            "left_d_ties": int(tie_l.sum().item()), "right_d_ties": int(tie_r.sum().item()),
+            "checked_mismatch": int(mism.sum().item()), "checked_mismatch_unjustified": unjust,
+            "checked_agreement_vs_fused_single_gpu_pass": round(float((chk_ds == fused).float().mean().item()), 6)}
+
+
+def run_split_extras(sm, torch, dist, m, Lc, Rc, W, H, D, r, rank, world, dev, stream, backend, steps):
     """N > 1 only: one frame split over the ranks, d-slices (cfg4, d_max 256, MIN reduction of the slice keys,
     both collectives) and row bands (r-row halo, all-gather of uint8 bands); whole-job maps/s on the
-    max-over-ranks clock."""
+    max-over-ranks clock.  Lc / Rc: the SAME frame on every rank (seeded alike), checked against rank 0's
+    single-GPU map before the split is timed."""
     from gpu_stereo_matching_amd import sharding
     D4 = 256
     keys, dflat = sharding.dslice_buffers(H, W, world, dev)
@@ -400,10 +516,11 @@ def run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, s
     n = max(10, steps // 4)
     dslice = {"config": f"cfg4: {W}x{H} d_max={D4} r={r}, one frame d-sharded over {world} ranks",
               "unit": "disparity-maps/s", "scaling": "strong", "keys_bytes_per_frame": W * H * 4}
+    dslice["check"] = split_parity_box(sm, torch, dist, m, Lc, Rc, r, D4, rank, world, dev, stream)
     for coll, label in (("rs_ag", f"reduce_scatter MIN int32 + all_gather uint8 ({backend})"),
                         ("allreduce", f"all_reduce MIN int32 ({backend})")):
         def dstep():
-            sharding.match_dslice(m, Lt[0], Rt[0], r, D4, rank, world, keys_t=keys, out_t=dflat, stream=stream,
+            sharding.match_dslice(m, Lc, Rc, r, D4, rank, world, keys_t=keys, out_t=dflat, stream=stream,
                                   collective=coll)
 
         for _ in range(5):
@@ -421,8 +538,21 @@ def run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, s
                         "collective": label}
 
     # row bands of one frame (r-row halo, all-gather of uint8 bands)
+    # row bands: the same frame, checked like the d-slice before timing
+    ref = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    if rank == 0:
+        m.match_device(Lc, Rc, r, D, out_t=ref, stream=stream)
+        torch.cuda.synchronize(dev)
+    dist.broadcast(ref, 0)
+    got = sharding.match_rowband(m, Lc, Rc, r, D, rank, world, out_t=d1, stream=stream)
+    torch.cuda.synchronize(dev)
+    bad = torch.tensor([float((got != ref).sum().item())], dtype=torch.float64, device=dev)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    band_check = {"parity": int(bad.item()) == 0, "rule": "bit-exact vs rank 0's single-GPU map, every rank",
+                  "mismatching_pixels_max_over_ranks": int(bad.item())}
+
     def bstep():
-        sharding.match_rowband(m, Lt[0], Rt[0], r, D, rank, world, out_t=d1, stream=stream)
+        sharding.match_rowband(m, Lc, Rc, r, D, rank, world, out_t=d1, stream=stream)
 
     for _ in range(5):
         bstep()
@@ -437,7 +567,7 @@ def run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, s
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     rowband = {"value": round(n / float(dt.item()), 2), "unit": "disparity-maps/s",
                "ms_per_frame": round(float(dt.item()) * 1000 / n, 4), "collective": f"all_gather uint8 bands ({backend})",
-               "halo_rows": r, "scaling": "strong"}
+               "halo_rows": r, "scaling": "strong", "check": band_check}
 
     return dslice, rowband
 
@@ -533,10 +663,17 @@ def main():
         lat = e0.elapsed_time(e1) / 50
 
     # ---- d-slice sharding of one frame (N > 1): cfg4, 1080p d_max=256, MIN reduction of the slice keys ----
-    dslice = rowband = None
+    dslice = rowband = inventory = None
     if distributed:
         try:
-            dslice, rowband = run_split_extras(sm, torch, dist, m, Lt, Rt, W, H, D, r, rank, world, dev, stream,
+            inventory = rank_inventory(torch, dist, dev, backend)
+        except Exception as e:  # report, never hide
+            inventory = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            # one common frame (the same seed on every rank), not this rank's Lt[0]
+            Lc_np, Rc_np = sm.synth_pair(args.seed, W, H, 256)
+            Lc, Rc = torch.from_numpy(Lc_np).to(dev), torch.from_numpy(Rc_np).to(dev)
+            dslice, rowband = run_split_extras(sm, torch, dist, m, Lc, Rc, W, H, D, r, rank, world, dev, stream,
                                                backend, args.steps)
         except Exception as e:  # report, never hide; the headline above is already measured
             dslice = {"error": f"{type(e).__name__}: {e}"}
@@ -587,9 +724,13 @@ def main():
                     m5.set_guided_eps(1e-4 * 255 * 255)
                     kb5 = sharding.dslice_buffers(H5, W5, world, dev)
                     rb5 = sharding.dslice_buffers(H5, W5, world, dev)
+                    # the same frame on every rank (seed 4321, frame 0 of rank 0's batch)
+                    Lc5_np, Rc5_np = sm.synth_pair(4321, W5, H5, D5)
+                    Lc5, Rc5 = torch.from_numpy(Lc5_np).to(dev), torch.from_numpy(Rc5_np).to(dev)
+                    chk5 = split_parity_guided_lr(sm, torch, dist, m5, Lc5, Rc5, r, D5, rank, world, dev, stream)
 
                     def dstep5():
-                        sharding.match_dslice(m5, L5[0], R5[0], r, D5, rank, world, keys_t=kb5[0], out_t=kb5[1],
+                        sharding.match_dslice(m5, Lc5, Rc5, r, D5, rank, world, keys_t=kb5[0], out_t=kb5[1],
                                               stream=stream, agg="guided", lr_check=True, right_bufs=rb5)
 
                     for _ in range(2):
@@ -608,7 +749,7 @@ def main():
                                   f"left + right slice keys, two MIN reduce_scatter int32 + two all_gather uint8 "
                                   f"({backend}), LR check", "value": round(n5 / float(t.item()), 2),
                         "unit": "disparity-maps/s", "ms_per_frame": round(float(t.item()) * 1000 / n5, 4),
-                        "scaling": "strong", "keys_bytes_per_frame": W5 * H5 * 8}
+                        "scaling": "strong", "keys_bytes_per_frame": W5 * H5 * 8, "check": chk5}
                 except Exception as e:  # report, never hide
                     cfg5["dslice_guided_lr"] = {"error": f"{type(e).__name__}: {e}"}
         finally:
@@ -667,6 +808,11 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
         }
+        if inventory is not None:
+            res["rccl_world"] = inventory
+            checks = [c.get("check", {}).get("parity") for c in (dslice or {}, rowband or {})]
+            checks.append(((cfg5 or {}).get("dslice_guided_lr") or {}).get("check", {}).get("parity"))
+            res["split_parity"] = all(c is True for c in checks) if None not in checks else None
         if dslice is not None:
             res["dslice"] = dslice
         if rowband is not None:

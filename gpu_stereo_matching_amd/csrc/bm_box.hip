@@ -498,9 +498,9 @@ void box_match_kernel(MatchArgs a, int tiles_x, int tiles_y) {
 // The LR check then runs on 4 pixels per thread with dword loads and stores where the rows allow.
 // Slice mode (rkeys != nullptr, multi-GPU d-slices with LR): the partial rows of a pass over d in
 // [d_lo, d_hi) hold u' = u + d_lo (box_match_kernel's right rows), `d_hi` is then the span d_hi - d_lo, and
-// the kernel writes the raw minimum key of every right pixel u to rkeys[f][y][u] (0x7FFFFFFF where no d of
-// the slice has u + d < W) instead of dR: keys of disjoint slices combine with a MIN (below 2^31 at r <= 15,
-// so signed and unsigned agree).
+// the kernel writes the minimum key of every right pixel u to rkeys[f][y][u], sign bit flipped (kRightKeyFlip;
+// 0x7FFFFFFF where no d of the slice has u + d < W), instead of dR: keys of disjoint slices combine with a
+// signed MIN.
 template <int MAXT>
 __global__ __launch_bounds__(256) void right_reduce_lr_vec_kernel(const uint32_t* __restrict__ rpart, int tiles_x,
                                                                   int tiles_y, int TW, int PWP, int dmax, int d_hi,
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(256) void right_reduce_lr_vec_kernel(const uint32_t
             const uint32_t kk[4] = {k0, k1, k2, k3};
 #pragma unroll
             for (int b = 0; b < 4; ++b)
-                if (u + b < W && u + b >= d_lo) krow[u + b - d_lo] = kk[b];
+                if (u + b < W && u + b >= d_lo) krow[u + b - d_lo] = kk[b] ^ kRightKeyFlip;
             continue;
         }
         const uint32_t dr4 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(k3, k2, 0x0C0C0400u),

@@ -87,8 +87,14 @@ hipError_t launch_volume_wta(const uint16_t* sad, int W, int H, int D, int frame
 // radius 16..127 (bm_wide.hip): V planes (u16, (d_hi - d_lo) * W * H per frame of a launch group, in `ws`,
 // wide_workspace_bytes) then one block per image row; a.valid_mode 0, 4 <= W <= 4096.  right (optional): the right view's dR [batch][H][rpitch]
 size_t wide_workspace_bytes(int W, int H, int D, int batch);
+// rkeys (d-slices with LR): the right view's raw keys [batch][H][W] of the slice [a.d_lo, a.d_hi), sign bit flipped
+// (kRightKeyFlip), instead of / beside `right`
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
-                                 int64_t rstride, hipStream_t s);
+                                 int64_t rstride, hipStream_t s, uint32_t* rkeys = nullptr);
+// Box right-view slice keys carry the sign bit flipped: (cost << 8 | d) ^ 2^31, so that a signed MIN orders them
+// like the unsigned keys at every radius (a wide window's key reaches 255 * 255^2 << 8 > 2^31 from r = 91), and
+// "no d of the slice reaches u" (0xFFFFFFFF before the flip) is INT32_MAX, as for the guided keys.
+constexpr uint32_t kRightKeyFlip = 0x80000000u;
 constexpr int kMaxWideWidth = 4096;
 // radius 16..127, 4 <= W <= 4096 and frames below 2^31 bytes (its buffer loads address a frame with 32-bit
 // offsets) take the separable wide-window path (bm_wide.hip); the rest the generic kernel

@@ -101,7 +101,8 @@ __device__ __forceinline__ void vsum_walk(const uint8_t* __restrict__ L, const u
             so += y + k <= pe ? o : z;
         }
     }
-    const bool full = c4 + 4 <= W;
+    // 8-B vector store only where the row start keeps it 8-B aligned (W % 4 == 0), else per column
+    const bool full = c4 + 4 <= W && (W & 3) == 0;
     constexpr int kU = 8;   // 4 and 16 measured the same (profiles/microbench/r05_wide_path.txt)
     // one batch of kU rows: the kU entering and kU leaving rows, clamped into the frame, loaded together
     // (4 kU loads in flight), then the sums; EDGE batches (a row entering past H or leaving above 0,
@@ -179,6 +180,7 @@ struct WideOut {
     uint8_t* right;   // right view (or null)
     int rpitch;
     int64_t rfs;
+    uint32_t* rkeys;  // d-slice right keys [frame][H][W], sign bit flipped (or null)
 };
 
 // One block per image row, grid (H, frames of the group).
@@ -202,10 +204,11 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
     uint8_t* __restrict__ disp = out.disp ? out.disp + g * out.ofs : nullptr;
     uint32_t* __restrict__ keys = out.keys ? out.keys + (int64_t)g * W * H : nullptr;
     uint8_t* __restrict__ right = out.right ? out.right + g * out.rfs : nullptr;
+    uint32_t* __restrict__ rkeys = out.rkeys ? out.rkeys + (int64_t)g * W * H : nullptr;
     const int opitch = out.opitch, rpitch = out.rpitch;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int x0 = t * NPT;
-    const bool want_right = right != nullptr;
+    const bool want_right = right != nullptr || rkeys != nullptr;
     if (want_right)
         for (int i = t; i < NPAD; i += NT) rmin[i] = 0xFFFFFFFFu;   // indexed pad(u), as pref
     uint32_t best[NPT];
@@ -313,7 +316,10 @@ __global__ __launch_bounds__(NT) void wide_hwta_kernel(const uint16_t* __restric
         if (x < W) {
             if (disp) disp[(int64_t)y * opitch + x] = best[k] < thresh ? (uint8_t)(best[k] & 0xFFu) : (uint8_t)0;
             if (keys) keys[(int64_t)y * W + x] = best[k];
-            if (want_right) right[(int64_t)y * rpitch + x] = (uint8_t)(rmin[pad(x)] & 0xFFu);   // no threshold
+            if (right) right[(int64_t)y * rpitch + x] = (uint8_t)(rmin[pad(x)] & 0xFFu);   // no threshold
+            // slice keys: (cost << 8 | d) of the slice's best d for u = x (0xFFFFFFFF where no d of the slice has
+            // x + d < W), sign bit flipped
+            if (rkeys) rkeys[(int64_t)y * W + x] = rmin[pad(x)] ^ kRightKeyFlip;
         }
     }
 }
@@ -322,7 +328,7 @@ template <int NPT, int NT>
 hipError_t launch_h(const uint16_t* V, int W, int H, int radius, int d_lo, int d_hi, uint32_t seed, uint32_t thresh,
                     const WideOut& out, int frames, hipStream_t s) {
     constexpr int NX = NT * NPT + 1;
-    const size_t lds = (size_t)((out.right ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
+    const size_t lds = (size_t)((out.right || out.rkeys ? 3 : 2) * (NX + NX / 8 + 1)) * 4;
     hipLaunchKernelGGL((wide_hwta_kernel<NPT, NT>), dim3((unsigned)H, (unsigned)frames), dim3(NT), lds, s, V, W, H,
                        radius, d_lo, d_hi, seed, thresh, out);
     return hipGetLastError();
@@ -355,7 +361,7 @@ size_t wide_workspace_bytes(int W, int H, int D, int batch) {
 }
 
 hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, uint8_t* right, int rpitch,
-                                 int64_t rstride, hipStream_t s) {
+                                 int64_t rstride, hipStream_t s, uint32_t* rkeys) {
     if (!wide_path(kMaxBoxRadius + 1, a.W, a.H, a.pitch) || a.valid_mode != 0 || a.d_hi <= a.d_lo || batch <= 0)
         return hipErrorInvalidValue;
     const int nd = a.d_hi - a.d_lo;
@@ -387,6 +393,7 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
         out.right = right ? right + (int64_t)f * rstride : nullptr;
         out.rpitch = rpitch;
         out.rfs = rstride;
+        out.rkeys = rkeys ? rkeys + (int64_t)f * a.W * a.H : nullptr;
         if (a.W <= 1024)
             e = launch_span<1024>(ws, a.W, a.H, a.radius, a.d_lo, a.d_hi, a.seed_key, a.thresh_key, out, n, s);
         else if (a.W <= 2048)

@@ -228,9 +228,10 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
 // Core device-side pass over `batch` frames.  Workspace planes (d_lr) are dense W x H frames.
 //   left map  : matched straight into `disp`, or into a workspace plane when SM_MEDIAN filters it
 //               into `disp` afterwards (StereoDisparity.cpp:85/119);
-//   right map : fused with the left pass for box r <= 7 and for guided (right keys from
-//               the left costs, bm_guided.hip); box r > 7 matches the mirrored pair (valid d <= x,
-//               no threshold) and keeps it mirrored;
+//   right map : fused with the left pass for box r <= 15 and for guided (right keys from
+//               the left costs, bm_guided.hip); box r = 16..127 takes it from the wide kernel's LDS
+//               atomic-min row (bm_wide.hip); only frames the wide path rejects (W > 4096, or planes of
+//               2^31 bytes and up) match the mirrored pair (valid d <= x, no threshold), kept mirrored;
 //   LR check  : StereoDisparity.cpp:136-147 on the (median-filtered, :119-126) maps.
 int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                     int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
@@ -366,9 +367,10 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
 
 // run_device_body on stream s, ordered after the handle's previous pass when that ran on another
 // stream (the workspaces d_lr / d_rpart / d_vol are per handle).
-// A pass without median, LR or staged volumes touches no workspace: it neither waits for nor records the
-// scratch event (round 4: the marker cost the host call ~µs; SM_SCRATCH_EVENT=1, read once, keeps both for
-// every pass, for A/B)
+// A pass without median, LR, staged volumes or the wide path's V planes touches no workspace: it neither
+// waits for nor records the scratch event (round 4: the marker cost the host call ~µs; SM_SCRATCH_EVENT=1,
+// read once, keeps both for every pass, for A/B).  A box pass at r 16..127 writes its V planes into d_vol
+// (and may grow it), so it is ordered like the others.
 bool scratch_event_forced() {
     static const bool on = [] {
         const char* e = getenv("SM_SCRATCH_EVENT");
@@ -381,7 +383,7 @@ int run_device(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
                int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
                uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
     const bool uses_ws = (flags & (SM_STAGED | SM_MEDIAN | SM_LR_CHECK | SM_DEVICE_CU_GRID)) != 0 || right_out || mask_out ||
-                         scratch_event_forced();
+                         (!(flags & SM_AGG_GUIDED) && sm::wide_path(radius, W, H, pitch)) || scratch_event_forced();
     if (uses_ws && h->scratch_pending && h->scratch_stream != s) SM_HIP(hipStreamWaitEvent(s, h->scratch_ev, 0));
     const int rc = run_device_body(h, L, R, W, H, pitch, batch, fstride, radius, D, flags, disp, opitch, ostride,
                                    right_out, mask_out, apitch, astride, s);
@@ -707,8 +709,8 @@ DslicePlan dslice_plan(int64_t P, int D, int n, int k, int H = 1) {
 
 // keys no d of the slice improves: the Device.cu:37 seed (box) / INT32_MAX (guided, signed keys)
 uint32_t dslice_none_key(int radius, bool guided) { return guided ? 0x7FFFFFFFu : seed_key(radius); }
-// right-view keys no d of the slice reaches (no seed: StereoHelper.cpp:131-154 has no threshold); box right
-// keys are < 2^31 at the fused right view's radii (255 * 31^2 << 8), so one value serves both MINs
+// right-view keys no d of the slice reaches (no seed: StereoHelper.cpp:131-154 has no threshold): INT32_MAX for
+// both aggregations, since box right keys are sign-flipped (kRightKeyFlip) and every right-key MIN is signed
 uint32_t dslice_none_rkey(bool) { return 0x7FFFFFFFu; }
 
 // One d-sliced frame: geometry, aggregation and whether the LR check runs (SM_LR_CHECK: a second key map
@@ -779,6 +781,12 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
             return SM_OK;
         }
         SM_HIP(sm::launch_box_match(a, 1, s));
+        return SM_OK;
+    }
+    if (sm::wide_path(radius, W, H, pitch)) {   // r 16..127: the wide path's right row, keys sign-flipped
+        int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo, 1));
+        if (rc) return rc;
+        SM_HIP(sm::launch_box_match_wide(a, 1, reinterpret_cast<uint16_t*>(h->d_vol), nullptr, 0, 0, s, rkeys));
         return SM_OK;
     }
     int rc = ensure_rpart(h, sm::box_right_partial_bytes(W, H, radius, d_hi - d_lo, 1));
@@ -886,9 +894,16 @@ int dslice_member_upload(sm_handle* h, int k, int n, const uint8_t* left, const 
     if (dslice_fault(k, "keys")) return fail(SM_ERR_LAUNCH, "d-slice member %d: injected fault (keys)", k);
     int rc = ensure_dsl(h, dslice_ws(nullptr, p, n, c.W, c.lr).bytes);
     if (rc) return rc;
-    if (c.lr && p.hi > p.lo) {   // the right view's per-tile partials, before any collective
+    const bool wide = !c.guided && sm::wide_path(c.radius, c.W, c.H, c.W);
+    if (c.lr && p.hi > p.lo && !wide) {   // the right view's per-tile partials, before any collective
         rc = ensure_rpart(h, c.guided ? sm::guided_right_partial_bytes(c.W, c.H, c.radius, p.hi - p.lo, 1)
                                       : sm::box_right_partial_bytes(c.W, c.H, c.radius, p.hi - p.lo, 1));
+        if (rc) return rc;
+    }
+    // a box slice at r 16..127 runs the wide path (right keys included), whose V planes live in d_vol: sized
+    // here too, so that its allocation cannot fail after the pair all-gathers are enqueued
+    if (wide && p.hi > p.lo) {
+        rc = ensure_vol(h, sm::wide_workspace_bytes(c.W, c.H, p.hi - p.lo, 1));
         if (rc) return rc;
     }
     const DsliceWs w = dslice_ws(h->d_dsl, p, n, c.W, c.lr);
@@ -934,7 +949,8 @@ int dslice_member_collect(sm_handle* h, const RcclApi* api, ncclComm_t* comm, Ds
     const ncclDataType_t kt = c.guided ? ncclInt32 : ncclUint32;
     if (api->reduce_scatter(w.keys, w.mine, (size_t)p.chunk, kt, ncclMin, *comm, s) != ncclSuccess)
         return bail(SM_ERR_LAUNCH, "ncclReduceScatter failed");
-    if (c.lr && api->reduce_scatter(w.rkeys, w.rmine, (size_t)p.chunk, kt, ncclMin, *comm, s) != ncclSuccess)
+    // right keys: signed for both aggregations (box right keys are sign-flipped, kRightKeyFlip)
+    if (c.lr && api->reduce_scatter(w.rkeys, w.rmine, (size_t)p.chunk, ncclInt32, ncclMin, *comm, s) != ncclSuccess)
         return bail(SM_ERR_LAUNCH, "ncclReduceScatter (right keys) failed");
     if (dslice_finalise(w.mine, p.chunk, c.radius, c.guided, w.mine8, s) ||
         (c.lr && sm::launch_keys_low_byte(w.rmine, p.chunk, w.rmine8, s) != hipSuccess))
@@ -1259,9 +1275,11 @@ SM_API int sm_slice_keys_lr_device(sm_handle* h, const uint8_t* d_left, const ui
     if ((flags & ~(unsigned)SM_AGG_GUIDED) != 0u)
         return fail(SM_ERR_INVALID_ARG, "slice LR keys: flags 0x%x (SM_AGG_BOX or SM_AGG_GUIDED)", flags);
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
-    if (radius > (guided ? sm::kMaxFastRadius : sm::kMaxBoxRadius))
-        return fail(SM_ERR_INVALID_ARG, "slice LR keys: radius %d > %d", radius,
-                    guided ? sm::kMaxFastRadius : sm::kMaxBoxRadius);
+    if (guided ? radius > sm::kMaxFastRadius
+               : radius > sm::kMaxBoxRadius && !sm::wide_path(radius, width, height, pitch))
+        return fail(SM_ERR_INVALID_ARG, "slice LR keys: radius %d > %d%s", radius,
+                    guided ? sm::kMaxFastRadius : sm::kMaxBoxRadius,
+                    guided ? "" : " outside the wide path (width 4..4096, frame < 2^31 bytes)");
     if (d_lo < 0 || d_hi <= d_lo || d_hi > sm::kMaxDisp)
         return fail(SM_ERR_INVALID_ARG, "bad slice [%d,%d)", d_lo, d_hi);
     if (!d_left || !d_right || !d_left_keys || !d_right_keys) return fail(SM_ERR_INVALID_ARG, "null device pointer");
@@ -1833,9 +1851,9 @@ SM_API int sm_group_dslice_block_match_u8(sm_group* g, const uint8_t* left, cons
                     "d-slice mode: flags 0x%x (box or SM_AGG_GUIDED, optionally SM_LR_CHECK; no median, staged)", flags);
     const bool guided = (flags & SM_AGG_GUIDED) != 0;
     const DsliceCfg cfg{width, height, radius, num_disp, guided, (flags & SM_LR_CHECK) != 0};
-    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius)
-        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d (the fused right view)", radius,
-                    sm::kMaxBoxRadius);
+    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius && !sm::wide_path(radius, width, height, width))
+        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d needs the wide path (width <= %d)", radius,
+                    sm::kMaxBoxRadius, sm::kMaxWideWidth);
     for (GroupWorker* w : g->w) {
         int rc = check_geometry(w->h, width, height, width, radius, num_disp);
         if (rc) return rc;
@@ -1902,9 +1920,9 @@ SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_
     if (guided && radius > sm::kMaxFastRadius)
         return fail(SM_ERR_INVALID_ARG, "guided aggregation: radius %d > %d", radius, sm::kMaxFastRadius);
     const DsliceCfg cfg{width, height, radius, num_disp, guided, (flags & SM_LR_CHECK) != 0};
-    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius)
-        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d (the fused right view)", radius,
-                    sm::kMaxBoxRadius);
+    if (cfg.lr && !guided && radius > sm::kMaxBoxRadius && !sm::wide_path(radius, width, height, width))
+        return fail(SM_ERR_INVALID_ARG, "d-slice LR: box radius %d > %d needs the wide path (width <= %d)", radius,
+                    sm::kMaxBoxRadius, sm::kMaxWideWidth);
     if (width > h->max_w || height > h->max_h || num_disp > h->max_d)
         return fail(SM_ERR_CAPACITY, "frame %dx%d/D=%d exceeds handle capacity", width, height, num_disp);
     const int64_t P = (int64_t)width * height;
@@ -1935,19 +1953,17 @@ SM_API int sm_dslice_rehearse_u8(sm_handle* h, const uint8_t* left, const uint8_
         rc = dslice_keys(h, dslice_plan(P, num_disp, n, k, height), cfg, ws.gl, ws.gr, keys_of(k), rkeys_of(k), s);
         if (rc) return rc;
     }
-    // the reduce-scatter's MIN (into member 0's buffers: signed for guided keys, unsigned for box keys,
-    // whose right-view keys carry no seed), then each member's chunk finalised into the all-gather's slot k
+    // the reduce-scatter's MIN (into member 0's buffers: left keys signed for guided, unsigned for box; right
+    // keys signed for both, box ones being sign-flipped), then each member's chunk finalised into slot k
     for (int k = 1; k < n; ++k) {
-        if (guided) {
+        if (guided)
             SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.keys), reinterpret_cast<const int*>(keys_of(k)),
                                        p0.padded, s));
-            if (cfg.lr)
-                SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.rkeys), reinterpret_cast<const int*>(rkeys_of(k)),
-                                           p0.padded, s));
-        } else {
+        else
             SM_HIP(sm::launch_min_keys_u32(ws.keys, keys_of(k), p0.padded, s));
-            if (cfg.lr) SM_HIP(sm::launch_min_keys_u32(ws.rkeys, rkeys_of(k), p0.padded, s));
-        }
+        if (cfg.lr)
+            SM_HIP(sm::launch_min_keys(reinterpret_cast<int*>(ws.rkeys), reinterpret_cast<const int*>(rkeys_of(k)),
+                                       p0.padded, s));
     }
     for (int k = 0; k < n; ++k) {
         const DslicePlan p = dslice_plan(P, num_disp, n, k, height);

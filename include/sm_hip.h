@@ -176,10 +176,11 @@ SM_API int sm_guided_keys_to_disp_device(sm_handle *h, const int32_t *d_keys, in
  * uint32) or sm_guided_slice_keys_device (SM_AGG_GUIDED, int32), and d_right_keys the right view's keys,
  * C_R(y, u, d) = C_L(y, u + d, d) (StereoHelper.cpp:156-180): per right pixel the minimum over d in
  * [d_lo, d_hi) with u + d < W of (cost << 8) | d, no threshold (:131-154); box: (SAD << 8 | d), guided:
- * (floor(q * 2^14) << 8 | d); INT32_MAX where no d of the slice reaches u.  Box keys (left and right) are
- * below 2^31 at these radii, so right keys of disjoint slices combine with the same elementwise MIN as the
- * left keys, signed or unsigned (guided: signed).  radius <= 15 (box) / <= 7 (guided).  Uses the handle's
- * right-view workspace. */
+ * (floor(q * 2^14) << 8 | d); INT32_MAX where no d of the slice reaches u.  Box right keys carry the sign bit
+ * flipped, (SAD << 8 | d) ^ 0x80000000, because a wide window's key passes 2^31 from r = 91: right keys of
+ * disjoint slices combine with a SIGNED elementwise MIN for both aggregations (box left keys: unsigned, as
+ * sm_slice_keys_device's; guided left keys: signed).  Box radius <= 15 (fused right view) or 16..127 through
+ * the wide path (width 4..4096); guided radius <= 7.  Uses the handle's right-view / volume workspace. */
 SM_API int sm_slice_keys_lr_device(sm_handle *h, const uint8_t *d_left, const uint8_t *d_right, int width, int height,
                                    int pitch, int radius, int d_lo, int d_hi, unsigned flags, void *d_left_keys,
                                    void *d_right_keys, void *stream);
@@ -346,7 +347,7 @@ SM_API int sm_group_block_match_batch_u8(sm_group *g, const uint8_t *const *left
  * differently from a single pass.  flags: 0 (box) or SM_AGG_GUIDED, optionally | SM_LR_CHECK: each
  * member also emits the right view's keys for its slice from the same fused pass
  * (sm_slice_keys_lr_device), a second MIN reduce-scatter + all-gather forms dR, and member 0 applies
- * StereoDisparity.cpp:136-147 before the download (box LR: radius <= 15).  Members must be distinct
+ * StereoDisparity.cpp:136-147 before the download (box LR: any radius the wide path takes).  Members must be distinct
  * devices; RCCL (librccl.so.1) is loaded on first use and one communicator per member is created
  * with ncclCommInitAll.
  * Failure handling: the call runs in two phases.  Phase 1 (upload, slice keys, stream sync) runs on

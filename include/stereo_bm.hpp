@@ -189,7 +189,8 @@ inline int block_matching(const M& h_left, const M& h_right, M& h_disparity, int
     const bool dslice = e.g && mode && std::string(mode) == "dslice" && (flags & ~(unsigned)SM_AGG_GUIDED) == 0u;
     // the stage lines read the upload / match / download split of this call only: the handle stays at the
     // auto default (no event markers) for testBM / getDisp / PreCal / getAllSAD
-    const bool timed = stage_lines && !detail::quiet() && !e.g;
+    // (a literal SM_DEVICE_CU_GRID call runs on e.h even when a group exists, so it is timed there: ADVICE r5)
+    const bool timed = stage_lines && !detail::quiet() && (!e.g || (flags & SM_DEVICE_CU_GRID));
     if (timed) sm_set_param_f(e.h, SM_PARAM_STAGE_TIMING, 1.f);
     const auto t0 = std::chrono::steady_clock::now();
     // Device.cu's literal launch geometry (SM_DEVICE_CU_GRID) is a whole-frame pass: one device

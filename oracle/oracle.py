@@ -224,18 +224,20 @@ def box_keys_slice(left, right, radius: int, d_lo: int, d_hi: int) -> np.ndarray
 def box_right_keys_slice(left, right, radius: int, d_lo: int, d_hi: int, cost: np.ndarray = None) -> np.ndarray:
     """Right-view d-slice keys (the contract of sm_slice_keys_lr_device's right map, box): for right pixel u
     the minimum over d in [d_lo, d_hi) with u + d < W of (C_L(u + d, d) << 8 | d), C_R(u, d) = C_L(u + d, d)
-    (StereoHelper.cpp:156-180), 0x7FFFFFFF where no d of the slice reaches u.  uint32 [H, W].  `cost`: a
-    box_cost volume of at least d_hi planes (computed when None)."""
+    (StereoHelper.cpp:156-180), with the sign bit flipped (^ 0x80000000: a wide window's key passes 2^31, and
+    the flip makes a signed MIN order the keys at every radius); 0x7FFFFFFF where no d of the slice reaches u.
+    uint32 bit patterns [H, W]: combine slices with a MIN on their int32 view.  `cost`: a box_cost volume of
+    at least d_hi planes (computed when None)."""
     if cost is None:
         cost = box_cost(left, right, radius, d_hi)
     _, H, W = cost.shape
-    best = np.full((H, W), 0x7FFFFFFF, np.int64)
+    best = np.full((H, W), 0xFFFFFFFF, np.int64)
     for d in range(d_lo, d_hi):
         if d >= W:
             break
         k = (cost[d][:, d:].astype(np.int64) << 8) | d
         best[:, :W - d] = np.minimum(best[:, :W - d], k)
-    return best.astype(np.uint32)
+    return (best ^ 0x80000000).astype(np.uint32)
 
 
 def right_wta(cost: np.ndarray) -> np.ndarray:

@@ -80,13 +80,14 @@ def _lr_worker(rank, world, port, W, H, r, D, result_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,D,W", [(2, 48, 90), (3, 37, 61), (4, 3, 50)])
-def test_dslice_lr_reduction_gloo(tmp_path, world, D, W):
+@pytest.mark.parametrize("world,D,W,r", [(2, 48, 90, 3), (3, 37, 61, 3), (4, 3, 50, 3), (2, 40, 90, 40),
+                                         (3, 24, 70, 100)])
+def test_dslice_lr_reduction_gloo(tmp_path, world, D, W, r):
     """d-slices with the LR check (a second packed reduction for the right view): the right
     view's slice keys take the same MIN collectives, their d fields form dR, and StereoDisparity.cpp:136-147
     gives the single pass's checked map (box_lr) on every rank, through both collectives, with empty slices
-    (world 4 > D 3) and padded pixel counts."""
-    H, r = 30, 3
+    (world 4 > D 3), padded pixel counts and wide windows (r = 40, 100: the wide path's radii)."""
+    H = 30
     port = _free_port()
     mp.spawn(_lr_worker, args=(world, port, W, H, r, D, str(tmp_path)), nprocs=world, join=True)
     from oracle import oracle as O
@@ -98,6 +99,25 @@ def test_dslice_lr_reduction_gloo(tmp_path, world, D, W):
             assert np.array_equal(np.load(tmp_path / f"lr{k}_{coll}.npy"), want), (k, coll)
 
 
+def test_right_keys_flip_orders_keys_past_2_31():
+    """A 255-vs-0 frame at r = 100: window sums reach 255 * 201^2 (> 2^23), so raw right keys (SAD << 8 | d) pass
+    2^31.  With the sign bit flipped a signed MIN over any partition still gives STMatching's right WTA, and
+    "no d reaches u" (INT32_MAX) stays above every key."""
+    from oracle import oracle as O
+    W, H, r, D = 210, 205, 100, 6
+    L = np.full((H, W), 255, np.uint8)
+    R = np.zeros((H, W), np.uint8)
+    R[:, ::7] = 9
+    cost = O.box_cost(L, R, r, D)
+    assert int(cost.max()) << 8 >= 1 << 31
+    want = O.right_wta(cost)
+    for cuts in ((0, D), (0, 2, D), (0, 1, 3, 5, D)):
+        parts = [O.box_right_keys_slice(L, R, r, a, b, cost).view(np.int32) for a, b in zip(cuts, cuts[1:])]
+        k = np.minimum.reduce(parts)
+        assert np.array_equal((k & 0xFF).astype(np.uint8), want), cuts
+        assert (k < np.iinfo(np.int32).max).all()
+
+
 def test_right_keys_slice_min_is_right_wta():
     """The right view's slice keys MIN'ed over any partition of [0, D) give STMatching's right WTA
     (StereoHelper.cpp:131-180: the clamped walk, strict < from d = 0) on the oracle's cost volume."""
@@ -106,7 +126,8 @@ def test_right_keys_slice_min_is_right_wta():
     cost = O.box_cost(L, R, 2, 32)
     want = O.right_wta(cost)
     for cuts in ((0, 32), (0, 5, 32), (0, 1, 2, 17, 31, 32)):
-        k = np.minimum.reduce([O.box_right_keys_slice(L, R, 2, a, b, cost) for a, b in zip(cuts, cuts[1:])])
+        k = np.minimum.reduce([O.box_right_keys_slice(L, R, 2, a, b, cost).view(np.int32)
+                               for a, b in zip(cuts, cuts[1:])])
         assert np.array_equal((k & 0xFF).astype(np.uint8), want), cuts
 
 

@@ -98,21 +98,29 @@ def test_guided_slice_lr_keys(single, oracle, gray, cuts):
     assert ok_r.all(), f"right: {int((~ok_r).sum())} pixels outside the tie-aware tolerance"
     assert (right == rd_o).mean() > 0.99
     assert np.array_equal(chk, oracle.lr_check(left, right)[0])
-    # the same split through the one-call rehearsal, against the single pass (near-ties aside)
+    # the same split through the one-call rehearsal: every pixel of its checked map is the LR rule applied
+    # to some left and right disparities that each pass the tie-aware rule (no bare ratio)
+    from guided_check import tie_aware_lr_check
     reh = single.dslice_rehearse(L, R, r, D, len(cuts) - 1, agg="guided", lr_check=True)
-    assert (reh == single.match(L, R, r, D, agg="guided", lr_check=True)).mean() > 0.995
+    ref = {"disp": disp_o, "best": best, "q": q, "rdisp": rd_o, "cr": cr, "best_r": best_r}
+    ok = tie_aware_lr_check(reh, ref, D, W)
+    assert ok.all(), f"rehearsal: {int((~ok).sum())} checked pixels without a tie-aware justification"
+    assert np.array_equal(tie_aware_lr_check(chk, ref, D, W), np.ones_like(ok))
 
 
-def test_dslice_lr_group_one_rccl_member(single):
+def test_dslice_lr_group_one_rccl_member(single, oracle):
     """sm_group_dslice_block_match_u8 with SM_LR_CHECK through RCCL (one member on the one GPU):
-    two reduce-scatters, two all-gathers and member 0's LR check give the single pass's map."""
+    two reduce-scatters, two all-gathers and member 0's LR check give the single pass's map (box), and a
+    guided checked map every pixel of which is tie-aware-justified against the fp64 oracle."""
     import gpu_stereo_matching_amd as sm
+    from guided_check import guided_reference, tie_aware_lr_check
     L, R = _pair(333, 97, 96, seed=5)
     with sm.BlockMatcherGroup([0], 512, 256, 256) as g:
         g.set_guided_eps(EPS)
         assert np.array_equal(g.match_dslice(L, R, 4, 96, lr_check=True), single.match(L, R, 4, 96, lr_check=True))
         got = g.match_dslice(L, R, 3, 48, agg="guided", lr_check=True)
-        assert (got == single.match(L, R, 3, 48, agg="guided", lr_check=True)).mean() > 0.995
+    ok = tie_aware_lr_check(got, guided_reference(oracle, L, R, 3, 48, EPS), 48, L.shape[1])
+    assert ok.all(), f"{int((~ok).sum())} checked pixels without a tie-aware justification"
 
 
 @pytest.mark.parametrize("coll", ["rs_ag", "allreduce"])
@@ -136,9 +144,43 @@ def test_dslice_lr_torch_one_rccl_rank(coll):
         dist.destroy_process_group()
 
 
-def test_dslice_lr_rejects_wide_box_radius(single):
-    """Box d-slices with LR need the fused right view (radius <= 15)."""
-    import gpu_stereo_matching_amd as sm
-    L, R = _pair(80, 40, 16)
-    with pytest.raises(sm.SMError):
-        single.dslice_rehearse(L, R, 16, 16, 2, lr_check=True)
+@pytest.mark.parametrize("r", [16, 40, 127])
+@pytest.mark.parametrize("members", [1, 2, 3, 5, 8])
+def test_dslice_rehearsal_box_lr_wide_radius(single, members, r):
+    """box d-slices with LR at r >= 16 take their right keys from the wide path's LDS
+    atomic-min row (bm_wide.hip), sign-flipped; the split equals the single LR pass bit for bit."""
+    W, H, D = 333, 97, 64
+    L, R = _pair(W, H, D, seed=members * 3 + r)
+    want = single.match(L, R, r, D, lr_check=True)
+    assert np.array_equal(single.dslice_rehearse(L, R, r, D, members, lr_check=True), want)
+
+
+def test_box_slice_lr_keys_wide_match_oracle(single):
+    """Wide-path slice keys with LR (r = 21 and r = 100) against the oracle's restatement, for slices starting
+    past d = 0 and past the frame's width; at r = 100 on a 255-vs-0 frame the raw right keys pass 2^31, so the
+    flipped keys' signed order is exercised."""
+    import torch
+    from oracle import oracle as O
+    for (W, H, r, D, cuts, flat) in ((150, 60, 21, 48, (0, 13, 48), False), (61, 40, 21, 100, (0, 70, 100), False),
+                                     (230, 210, 100, 8, (0, 3, 8), True)):
+        if flat:
+            L = np.full((H, W), 255, np.uint8)
+            R = np.zeros((H, W), np.uint8)
+            R[:, ::5] = 17
+        else:
+            L, R = _pair(W, H, D)
+        Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+        cost = O.box_cost(L, R, r, D)
+        if flat:
+            assert int(cost.max()) << 8 >= 1 << 31
+        parts = []
+        for a, b in zip(cuts, cuts[1:]):
+            lk, rk = single.slice_keys_lr_device(Lt, Rt, r, a, b)
+            torch.cuda.synchronize()
+            assert np.array_equal(lk.cpu().numpy().view(np.uint32), O.box_keys_slice(L, R, r, a, b)), (r, a, b)
+            want = O.box_right_keys_slice(L, R, r, a, b, cost)
+            got = rk.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want), (r, a, b, int((got != want).sum()))
+            parts.append(got.view(np.int32))
+        rd = (np.minimum.reduce(parts) & 0xFF).astype(np.uint8)
+        assert np.array_equal(rd, O.right_wta(cost)), r

@@ -98,8 +98,14 @@ def test_group_dslice_one_member_guided(single):
         g.set_guided_eps(EPS)
         got = g.match_dslice(L, R, r, D, agg="guided")
     want = single.match(L, R, r, D, agg="guided")
-    # the keys quantise q to 2^-14: equal except where two fp32 costs are that close
+    # the keys quantise q to 2^-14: equal except where two fp32 costs are that close, and every
+    # pixel within the tie tolerance of the fp64 oracle (no bare ratio)
     assert (got == want).mean() >= 0.998
+    from guided_check import tie_aware_check
+    from oracle import oracle as O
+    disp_o, q, best = O.guided_disp(L, R, r, D, EPS, want_q=True)
+    ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, D, W)
+    assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
 
 
 def test_group_dslice_rejects_repeated_device_and_flags():

@@ -42,11 +42,16 @@ def test_guided_art(matcher, oracle, gray, r, D):
     assert exact.mean() > 0.995
 
 
-def test_guided_golden(matcher, gray, guided_expected):
+def test_guided_golden(matcher, oracle, gray, guided_expected):
+    """The committed golden map; pixels that differ from it must be fp64 near-ties (tie-aware rule)."""
     L, R = gray["Art_/view1"], gray["Art_/view5"]
     got = matcher.match(L, R, 5, 64, agg="guided")
     want = guided_expected["Art_/r5/D64/disp"]
     assert (got == want).mean() > 0.995
+    disp_o, q, best = oracle.guided_disp(L, R, 5, 64, EPS, want_q=True)
+    assert np.array_equal(disp_o, want)
+    ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, 64, L.shape[1])
+    assert ok.all(), f"{int((~ok).sum())} pixels outside the tie-aware tolerance"
 
 
 @pytest.mark.parametrize("W,H,D,r", [(333, 77, 100, 4), (64, 20, 8, 1), (21, 13, 30, 2)])
@@ -228,10 +233,14 @@ def test_guided_dslice_one_rccl_rank(oracle, torch):
             m.set_guided_eps(EPS)
             Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
             full = m.match_device(Lt, Rt, r, D, agg="guided")
+            disp_o, q, best = oracle.guided_disp(L, R, r, D, EPS, want_q=True)
             for coll in ("rs_ag", "allreduce"):
                 got = sharding.match_dslice(m, Lt, Rt, r, D, 0, 1, collective=coll, agg="guided")
                 torch.cuda.synchronize()
-                assert (got.cpu().numpy() == full.cpu().numpy()).mean() > 0.998, coll
+                got = got.cpu().numpy()
+                assert (got == full.cpu().numpy()).mean() > 0.998, coll
+                ok, _ = tie_aware_check(got, q, {"disp": disp_o, "best": best}, D, W)
+                assert ok.all(), f"{coll}: {int((~ok).sum())} pixels outside the tie-aware tolerance"
     finally:
         dist.destroy_process_group()
 

@@ -328,6 +328,24 @@ def test_two_streams_one_handle(matcher, oracle, torch):
         assert np.array_equal(o.cpu().numpy(), w)
 
 
+def test_two_streams_one_handle_wide(matcher, oracle, torch):
+    """a plain box pass at r 16..127 (no LR, no median) writes the wide path's V planes into the
+    handle's volume workspace and may grow it; two streams on one handle are ordered, so both maps are
+    exact.  The second pair has the larger D, so its pass grows the workspace behind the first."""
+    r = 20
+    cfg = [(700, 300, 64, 71), (900, 400, 160, 72)]
+    pairs = [oracle.synth_pair(seed, W, H, D) for W, H, D, seed in cfg]
+    want = [oracle.box_disp(L, R, r, D) for (L, R), (_, _, D, _) in zip(pairs, cfg)]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    dev = [(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()) for L, R in pairs]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        outs = [matcher.match_device(dev[i][0], dev[i][1], r, cfg[i][2], stream=(s1, s2)[i]) for i in range(2)]
+        torch.cuda.synchronize()
+        for o, w in zip(outs, want):
+            assert np.array_equal(o.cpu().numpy(), w)
+
+
 def test_out_tensor_validation(matcher, torch):
     """a caller-supplied output of the wrong shape / dtype / device is a ValueError, never
     an out-of-bounds device write."""

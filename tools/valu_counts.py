@@ -11,21 +11,27 @@ import csv, glob, json, os, statistics, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CTRS = "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE"
 # name, kernel-name substring, driver args; workload = [W, H, D, r, frames per launch]
+# name, kernel-name substring (rocprof's demangled name), driver args, workload, mangled-name substring (the
+# symbol whose machine code tools/codeobj.py hashes into the entry: bench.py reports frac null when the library
+# it loads carries other code for that kernel)
 JOBS = (
     ("box_r5_1080p_d128_b128", "box_match_kernel<5, 128, false, 4>", ["--agg", "box", "--batch", "128"],
-     [1920, 1080, 128, 5, 128]),
-    ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false", ["--agg", "guided", "--batch", "32"], [1920, 1080, 128, 5, 32]),
+     [1920, 1080, 128, 5, 128], "box_match_kernelILi5ELi128ELb0ELi4E"),
+    ("guided_r5_1080p_d128_b32", "guided_fused_kernel<5, false", ["--agg", "guided", "--batch", "32"],
+     [1920, 1080, 128, 5, 32], "guided_fused_kernelILi5ELb0E"),
     ("guided_lr_r5_1080p_d128_b32", "guided_fused_kernel<5, true", ["--agg", "guided", "--lr", "--batch", "32"],
-     [1920, 1080, 128, 5, 32]),
+     [1920, 1080, 128, 5, 32], "guided_fused_kernelILi5ELb1E"),
     # box + LR: the right-view matcher and its reduce, from the same runs
     ("box_lr_r5_1080p_d128_b32", "box_match_kernel<5, 128, true", ["--agg", "box", "--lr", "--batch", "32"],
-     [1920, 1080, 128, 5, 32]),
+     [1920, 1080, 128, 5, 32], "box_match_kernelILi5ELi128ELb1E"),
     ("box_lr_reduce_1080p_d128_b32", "right_reduce_lr_vec_kernel", ["--agg", "box", "--lr", "--batch", "32"],
-     [1920, 1080, 128, 5, 32]),
+     [1920, 1080, 128, 5, 32], "right_reduce_lr_vec_kernel"),
 )
 # SM_VALU_JOBS=name1,name2: only those jobs
 if os.environ.get("SM_VALU_JOBS"):
     JOBS = tuple(j for j in JOBS if j[0] in os.environ["SM_VALU_JOBS"].split(","))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import codeobj  # noqa: E402
 
 
 # issue / wait breakdown of the guided kernels: wave cycles spent waiting at
@@ -39,7 +45,8 @@ def main():
     tag = os.environ.get("SM_TAG", "")
     res = {"counters": CTRS.split(), "note": "chip totals per launch (median over launches); SQ_INSTS_VALU counts "
            "wave64 VALU instructions, SQ_LDS_IDX_ACTIVE LDS-array cycles summed over CUs", "kernels": {}}
-    for name, kname, args, wl in JOBS:
+    lib = os.environ.get("SM_LIB") or codeobj.default_lib()
+    for name, kname, args, wl, sym in JOBS:
         d = os.path.join(ROOT, "gpurun_out", "valu_counts" + tag, name)
         cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc"] + CTRS.split() + [
             "-d", d, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
@@ -70,7 +77,8 @@ def main():
             med["share_wait_any"] = med.get("SQ_WAIT_ANY", 0) / wc
             med["share_wait_inst_any"] = med.get("SQ_WAIT_INST_ANY", 0) / wc
             med["share_active_inst_any"] = med.get("SQ_ACTIVE_INST_ANY", 0) / wc
-        res["kernels"][name] = {"kernel": kname, "workload": wl, "per_launch": med}
+        res["kernels"][name] = {"kernel": kname, "workload": wl, "per_launch": med, "code_symbol": sym,
+                                "code_sha256": codeobj.kernel_sha256(lib, sym)}
         print(name, json.dumps(med), flush=True)
     out = os.path.join(ROOT, "gpurun_out", "valu_counts%s.json" % tag)
     json.dump(res, open(out, "w"), indent=1)
