@@ -92,6 +92,27 @@ constexpr uint32_t kPLow = kPOne - 1;
 #endif
 constexpr bool kGuidedRoles = SM_G_ROLES != 0;
 
+// SM_G_ACC (round 6, default 1): S1H's window sums of the packed columns without unpacking SIp per column (s1h
+// below): 152 -> 142 VALU per wave and d, 459.9 -> 452.9 us per 1080p guided frame, guided + LR 511.1 -> 505.0,
+// maps bit-identical (profiles/microbench/r06_guided_acc_pk_ab.txt).  0 keeps the unpacking form for A/B.
+// Not kept (same file): S2V's (a, b) running sums as v_pk_add_f32 pairs, 100 -> 50 VALU but 462.1 us (+0.5 %):
+// a packed f32 add costs the SIMD about what the two adds it replaces do.
+#ifndef SM_G_ACC
+#define SM_G_ACC 1
+#endif
+
+// SM_G_MARK=1 (analysis builds only, tools/isa_stage_mix.py): an assembly comment at each stage's entry and exit,
+// so the per-stage VALU mix can be read from the ISA.  The empty asm statements also act as scheduling
+// barriers, so the marked build is for counting, not for timing.
+#ifndef SM_G_MARK
+#define SM_G_MARK 0
+#endif
+#if SM_G_MARK
+#define G_MARK(tag) asm volatile(";@stage " tag ::: "memory")
+#else
+#define G_MARK(tag) ((void)0)
+#endif
+
 // Taller tiles (round 4: 48 rows on 6 waves, 96 rows on one 12-wave workgroup per CU) cut the halo but
 // lost occupancy and ran 1.9x / 1.3x slower; the variants were removed in round 5
 // (git history: SM_G_TALL / SM_G_TALL_RIGHT before commit "guided: drop the measured tall-tile variants").
@@ -370,9 +391,9 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     // S1H's constants as SGPR operands: the compiler would fold them into literal operands, whose 64-bit
     // encodings issue slower than the 32-bit VOP2 form with an SGPR source (38 ands, 9 ors and 9 adds
     // per wave and d)
-    uint32_t k_plow = kPLow, k_magic = 0x4B000000u;
+    uint32_t k_plow = kPLow, k_magic = 0x4B000000u, k_m2p20 = (uint32_t)-(int)kPOne;
     float k_magicf = -8388608.0f;
-    asm volatile("" : "+s"(k_plow), "+s"(k_magic), "+s"(k_magicf));
+    asm volatile("" : "+s"(k_plow), "+s"(k_magic), "+s"(k_magicf), "+s"(k_m2p20));
     // S1H ownership: A row h1i, segment h1s (threads >= AH*NSEG1 idle in S1H)
     const bool h1_on = tid < G::AH * G::NSEG1;
     const int h1i = h1_on ? tid / G::NSEG1 : 0, h1s = h1_on ? tid % G::NSEG1 : 0;
@@ -470,6 +491,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     auto s1v = [&](int d, auto stats, auto nomask) {
         constexpr bool STATS = decltype(stats)::value;
         constexpr bool NOMASK = decltype(nomask)::value;
+        G_MARK("S1V");
         const bool m = STATS || NOMASK || (col_in && xc >= d);
         const uint8_t* rc = rb + (c + kBandChunk - (d & (kBandChunk - 1)));
         uint32_t rv[G::NV];
@@ -493,6 +515,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             }
             Tp[k % (2 * R + 1)] = T;
         }
+        G_MARK("end");
     };
     // ================= S1H =================
     auto s1h_stats = [&]() {
@@ -528,22 +551,42 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
     };
     auto s1h = [&]() {
         if (!h1_on) return;
+        G_MARK("S1H");
         const uint32_t* row = cs + h1i * G::CSS + h1s * G::SW1;
         // the whole segment is loaded before the first a/b store (the compiler cannot tell abp
         // from cs, so interleaved loads would each wait for the stores before them)
         uint32_t v[G::SW1 + 2 * R];
 #pragma unroll
         for (int k = 0; k < G::SW1 + 2 * R; ++k) v[k] = row[k];
+#if SM_G_ACC
+        // SM_G_ACC: the packed column sums are summed as they are (acc, wrapping u32) beside the exact Sp; the
+        // window's SIp < 2^23 is then acc - Sp * 2^20 (mod 2^32, exact), one v_mad_i32_i24 per output instead of
+        // an and + add per column
+        uint32_t sp = 0, acc = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * R; ++k) {
+            sp += v[k] >> 20;
+            acc += v[k];
+        }
+#else
         uint32_t sp = 0, sip = 0;
 #pragma unroll
         for (int k = 0; k < 2 * R; ++k) {
             sp += v[k] >> 20;
             sip += v[k] & k_plow;
         }
+#endif
 #pragma unroll
         for (int o = 0; o < G::SW1; ++o) {
+#if SM_G_ACC
+            sp += v[o + 2 * R] >> 20;
+            acc += v[o + 2 * R];
+            uint32_t sip;
+            asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(sip) : "v"(sp), "s"(k_m2p20), "v"(acc));
+#else
             sp += v[o + 2 * R] >> 20;
             sip += v[o + 2 * R] & k_plow;
+#endif
             // N*SIp - SI*Sp = N^2 cov(I, p), |.| < 2^30, exactly: every factor fits a signed 24-bit
             // operand (SIp <= 121 * 255^2 < 2^23), so v_mul_i32_i24 + v_mad_i32_i24 (written out: the
             // compiler otherwise turns one product into a quarter-rate v_mul_lo_u32)
@@ -560,12 +603,18 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                          : "v"(h1off), "v"(__builtin_bit_cast(double, make_float2(a, b))), "i"(8 * o)
                          : "memory");
             sp -= v[o] >> 20;
+#if SM_G_ACC
+            acc -= v[o];
+#else
             sip -= v[o] & k_plow;
+#endif
         }
+        G_MARK("end");
     };
     // ================= S2V =================
     auto s2v = [&]() {
         if (!v2_on) return;
+        G_MARK("S2V");
         // one ds_read_b64 per row (2 LDS cycles) instead of a merged ds_read2_b64 (8 cycles for the
         // same two rows, MI355X_MICROARCH.md LDS table): rows k and k + 5 share a base whose value the
         // compiler cannot relate to the others, and 5 rows (2160 B) exceed ds_read2's offset range
@@ -606,11 +655,13 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
                 sb -= v[r].y;
             }
         }
+        G_MARK("end");
     };
     // ================= S2H + WTA =================
     // LIM: some output of the tile can have d past its validity limit (tile-uniform; interior tiles skip the test)
     auto s2h = [&](int d, auto lim) {
         constexpr bool LIM = decltype(lim)::value;
+        G_MARK("S2H");
         constexpr int NR = G::SW2 + 2 * R;   // mm values read per plane
         float va[NR], vb[NR];
         if constexpr (G::SW2 % 2 == 0) {
@@ -664,6 +715,7 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
             sb -= vb[o];
         }
         chain_step(d);
+        G_MARK("end");
     };
 
     // S1V's cs stores and S1H's a/b stores are inline asm, which the compiler's wait-count pass does
