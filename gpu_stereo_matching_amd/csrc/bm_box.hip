@@ -48,6 +48,11 @@ constexpr int kWavesD = (kWideRight<RIGHT, R> && DMAX == 192) ? 6 : kWaves<RIGHT
 // r05_box_lr_paired_scatter_ab.txt)
 template <int R>
 constexpr bool kPairedScatter = (R != 3);
+// (round 6, VERDICT r5 item 4, not kept: a register window over two disparity pairs, whose NQ + 1 held values per
+// half-row are min'ed into the next pair's before one ds_min_u32 per u, NQ + 3 atomics per two pairs instead of
+// 2 NQ + 2.  Bit-exact, but the window needs ~179 VGPRs: at the 6-wave kernel's 168 it spilled 48 B per lane, and
+// box + LR ran 552 -> 757 us per 4K D=192 frame, 79.0 -> 138.0 us per 1080p frame with d_max 128 moved to 6 waves;
+// profiles/microbench/r06_box_lr_rwin_ab.txt)
 // radius 8..15 (WIDE): the packed u16 column sums still fit (<= (32 + 2r) * 255), the window sums do
 // not, so phase H keeps the two halves in separate u32 sums; the longer CS rows and the 2r+1-row
 // ring need more than 128 VGPRs (2 waves/SIMD)

@@ -25,7 +25,7 @@ JOBS = (
     ("box_lr_r5_1080p_d128_b32", "box_match_kernel<5, 128, true", ["--agg", "box", "--lr", "--batch", "32"],
      [1920, 1080, 128, 5, 32], "box_match_kernelILi5ELi128ELb1E"),
     ("box_lr_reduce_1080p_d128_b32", "right_reduce_lr_vec_kernel", ["--agg", "box", "--lr", "--batch", "32"],
-     [1920, 1080, 128, 5, 32], "right_reduce_lr_vec_kernel"),
+     [1920, 1080, 128, 5, 32], "right_reduce_lr_vec_kernelILi4E"),
 )
 # SM_VALU_JOBS=name1,name2: only those jobs
 if os.environ.get("SM_VALU_JOBS"):

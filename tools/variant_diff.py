@@ -22,6 +22,14 @@ with sm.BlockMatcher(0, 1920, 1080, 256) as m:
         chk, rd, mask = m.match_lr(L, R, r, 64, agg='guided')
         res[f'art_glr{{r}}'] = np.stack([chk, rd, mask])
     res['syn_g5'] = m.match(sL, sR, 5, 128, agg='guided')
+    # box + LR (the fused right view), d_max 128 and 192, several radii
+    import os as _os
+    if _os.environ.get('SM_DIFF_BOXLR'):
+        for r in (1, 4, 5, 6):
+            res[f'syn_blr{{r}}'] = np.stack(m.match_lr(sL, sR, r, 128))
+            res[f'syn_blr{{r}}_d192'] = np.stack(m.match_lr(sL, sR, r, 192))
+        res['art_blr5'] = np.stack(m.match_lr(L, R, 5, 64))
+        res['syn_blr5_d100'] = np.stack(m.match_lr(sL[:300, :777], sR[:300, :777], 5, 100))
 np.savez({out!r}, **res)
 """
     subprocess.run([sys.executable, "-c", code], check=True, timeout=300)
