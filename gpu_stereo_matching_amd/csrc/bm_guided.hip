@@ -624,24 +624,28 @@ __global__ __launch_bounds__(kT, (kGuidedWavesPerEU<R, RIGHT>)) void guided_fuse
         // warm-up rows, as an 8-row strip does without the roles: the float sums, and so the maps, are
         // the same bit for bit in every configuration (the right-view kernel runs without the roles at
         // r = 2, 6, 7, and the LR check pairs its left map with the left-only kernel's)
+        // (round 6, not kept: one running sum over the wave's whole 16-row strip, 100 -> 82 VALU per wave and d, ran
+        // 451.3 -> 457.2 us per 1080p guided frame, guided + LR 504.7 -> 528.6 and 2968 -> 3110 at 4K: fewer
+        // instructions, longer dependent chains; profiles/microbench/r06_guided_s2v_run_ab.txt)
+        constexpr int GS = 8;
         constexpr int NRW = G::RPS + 2 * R;
         float2 v[NRW];
 #pragma unroll
-        for (int k = 0; k < 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
+        for (int k = 0; k < GS + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
 #pragma unroll
-        for (int g = 0; g < G::RPS / 8; ++g) {
+        for (int g = 0; g < G::RPS / GS; ++g) {
             if (g > 0) {
 #pragma unroll
-                for (int k = 8 * g + 2 * R; k < 8 * g + 8 + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
+                for (int k = GS * g + 2 * R; k < GS * g + GS + 2 * R; ++k) v[k] = v2col[k % 5][(k / 5) * 5 * G::ABS];
             }
             float sa = 0.f, sb = 0.f;
 #pragma unroll
-            for (int k = 8 * g; k < 8 * g + 2 * R; ++k) {
+            for (int k = GS * g; k < GS * g + 2 * R; ++k) {
                 sa += v[k].x;
                 sb += v[k].y;
             }
 #pragma unroll
-            for (int r = 8 * g; r < 8 * g + 8; ++r) {
+            for (int r = GS * g; r < GS * g + GS; ++r) {
                 sa += v[r + 2 * R].x;
                 sb += v[r + 2 * R].y;
                 // mmA / mmB [(RPS v2g + r) * MSA + lane]: lane-consecutive, so ds_write_addtid_b32, with
