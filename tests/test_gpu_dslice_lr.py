@@ -184,3 +184,30 @@ def test_box_slice_lr_keys_wide_match_oracle(single):
             parts.append(got.view(np.int32))
         rd = (np.minimum.reduce(parts) & 0xFF).astype(np.uint8)
         assert np.array_equal(rd, O.right_wta(cost)), r
+
+
+@pytest.mark.parametrize("seed", list(range(12)))
+def test_fuzz_dslice_lr_any_radius(single, seed):
+    """Seeded fuzz of the d-slice split with LR over the whole radius range (fused right view r <= 15, the
+    wide path's right row 16..127): random size, D, member count and tie-heavy textures; the rehearsal equals
+    the single LR pass bit for bit, and the box right slice keys of one member equal the oracle's."""
+    import torch
+    from fuzz_util import fuzz_pair
+    from oracle import oracle as O
+    rng = np.random.default_rng(9000 + seed)
+    r = int(rng.choice([int(rng.integers(0, 16)), int(rng.integers(16, 128))]))
+    W = int(rng.integers(8, 400))
+    H = int(rng.integers(4, 160))
+    D = int(rng.integers(1, 257))
+    n = int(rng.integers(1, 9))
+    L, R = fuzz_pair(rng, W, H)
+    want = single.match(L, R, r, D, lr_check=True)
+    got = single.dslice_rehearse(L, R, r, D, n, lr_check=True)
+    assert np.array_equal(got, want), (r, W, H, D, n, int((got != want).sum()))
+    lo = int(rng.integers(0, D))
+    hi = int(rng.integers(lo + 1, D + 1))
+    Lt, Rt = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    lk, rk = single.slice_keys_lr_device(Lt, Rt, r, lo, hi)
+    torch.cuda.synchronize()
+    assert np.array_equal(lk.cpu().numpy().view(np.uint32), O.box_keys_slice(L, R, r, lo, hi)), (r, lo, hi)
+    assert np.array_equal(rk.cpu().numpy().view(np.uint32), O.box_right_keys_slice(L, R, r, lo, hi)), (r, lo, hi)
