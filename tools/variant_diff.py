@@ -22,14 +22,19 @@ with sm.BlockMatcher(0, 1920, 1080, 256) as m:
         chk, rd, mask = m.match_lr(L, R, r, 64, agg='guided')
         res[f'art_glr{{r}}'] = np.stack([chk, rd, mask])
     res['syn_g5'] = m.match(sL, sR, 5, 128, agg='guided')
-    # box + LR (the fused right view), d_max 128 and 192, several radii
     import os as _os
+    # box + LR (the fused right view), d_max 128 and 192, several radii
     if _os.environ.get('SM_DIFF_BOXLR'):
         for r in (1, 4, 5, 6):
             res[f'syn_blr{{r}}'] = np.stack(m.match_lr(sL, sR, r, 128))
             res[f'syn_blr{{r}}_d192'] = np.stack(m.match_lr(sL, sR, r, 192))
         res['art_blr5'] = np.stack(m.match_lr(L, R, 5, 64))
         res['syn_blr5_d100'] = np.stack(m.match_lr(sL[:300, :777], sR[:300, :777], 5, 100))
+    if _os.environ.get('SM_DIFF_WIDE'):
+        res['syn_w20'] = m.match(sL, sR, 20, 128)
+        res['syn_w127lr'] = np.stack(m.match_lr(sL, sR, 127, 128))
+        res['syn_w40_odd'] = m.match(sL[:77, :333], sR[:77, :333], 40, 100)
+        res['syn_w16_lr'] = np.stack(m.match_lr(sL[:500, :1001], sR[:500, :1001], 16, 64))
 np.savez({out!r}, **res)
 """
     subprocess.run([sys.executable, "-c", code], check=True, timeout=300)
