@@ -30,6 +30,13 @@ with sm.BlockMatcher(0, 1920, 1080, 256) as m:
             res[f'syn_blr{{r}}_d192'] = np.stack(m.match_lr(sL, sR, r, 192))
         res['art_blr5'] = np.stack(m.match_lr(L, R, 5, 64))
         res['syn_blr5_d100'] = np.stack(m.match_lr(sL[:300, :777], sR[:300, :777], 5, 100))
+    if _os.environ.get('SM_DIFF_BOX'):
+        for r in (0, 1, 2, 3, 4, 5, 6, 7, 9, 15):
+            res[f'syn_b{{r}}'] = m.match(sL, sR, r, 128)
+        res['syn_b5_d256'] = m.match(sL, sR, 5, 256)
+        res['syn_b5_odd'] = m.match(sL[:301, :777], sR[:301, :777], 5, 100)
+        for k in ('Art', 'Books', 'Dolls'):
+            res[f'mb_{{k}}_b4'] = m.match(g[f'{{k}}/view1'], g[f'{{k}}/view5'], 4, 64)
     if _os.environ.get('SM_DIFF_WIDE'):
         res['syn_w20'] = m.match(sL, sR, 20, 128)
         res['syn_w127lr'] = np.stack(m.match_lr(sL, sR, 127, 128))
