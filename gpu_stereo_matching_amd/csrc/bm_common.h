@@ -95,6 +95,12 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
 // like the unsigned keys at every radius (a wide window's key reaches 255 * 255^2 << 8 > 2^31 from r = 91), and
 // "no d of the slice reaches u" (0xFFFFFFFF before the flip) is INT32_MAX, as for the guided keys.
 constexpr uint32_t kRightKeyFlip = 0x80000000u;
+// radius 16..31 without the right view (bm_strip.hip): disparities across the lanes, vertical sums in registers,
+// no workspace; strip_path says whether a pass takes it (SM_WIDE_STRIP=0, read once, turns it off for A/B)
+constexpr int kStripMinRadius = 16;
+constexpr int kStripMaxRadius = 31;
+bool strip_path(const MatchArgs& a);
+hipError_t launch_box_match_strip(const MatchArgs& a, int batch, hipStream_t s);
 constexpr int kMaxWideWidth = 4096;
 // radius 16..127, 4 <= W <= 4096 and frames below 2^31 bytes (its buffer loads address a frame with 32-bit
 // offsets) take the separable wide-window path (bm_wide.hip); the rest the generic kernel

@@ -326,10 +326,15 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
     } else if (wide) {
-        int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D, batch));
-        if (rc) return rc;
-        SM_HIP(sm::launch_box_match_wide(a, batch, reinterpret_cast<uint16_t*>(h->d_vol), lr ? right_map : nullptr, W,
-                                         P, s));
+        // r 16..31 without the right view: the strip kernel (bm_strip.hip), no V-plane workspace
+        if (!lr && sm::strip_path(a)) {
+            SM_HIP(sm::launch_box_match_strip(a, batch, s));
+        } else {
+            int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D, batch));
+            if (rc) return rc;
+            SM_HIP(sm::launch_box_match_wide(a, batch, reinterpret_cast<uint16_t*>(h->d_vol), lr ? right_map : nullptr,
+                                             W, P, s));
+        }
     } else {
         SM_HIP(sm::launch_box_match(a, batch, s));
     }
@@ -774,6 +779,10 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
     a.thresh_key = seed_key(radius);
     a.keys = keys;
     if (!rkeys) {
+        if (sm::wide_path(radius, W, H, pitch) && sm::strip_path(a)) {   // r 16..31: the strip kernel (bm_strip.hip)
+            SM_HIP(sm::launch_box_match_strip(a, 1, s));
+            return SM_OK;
+        }
         if (sm::wide_path(radius, W, H, pitch)) {   // the wide-window path (bm_wide.hip)
             int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, d_hi - d_lo, 1));
             if (rc) return rc;

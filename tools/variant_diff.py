@@ -42,6 +42,8 @@ with sm.BlockMatcher(0, 1920, 1080, 256) as m:
         res['syn_w127lr'] = np.stack(m.match_lr(sL, sR, 127, 128))
         res['syn_w40_odd'] = m.match(sL[:77, :333], sR[:77, :333], 40, 100)
         res['syn_w16_lr'] = np.stack(m.match_lr(sL[:500, :1001], sR[:500, :1001], 16, 64))
+        res['syn_w16_d256'] = m.match(sL, sR, 16, 256)
+        res['syn_w31_odd'] = m.match(sL[:301, :1003], sR[:301, :1003], 31, 70)
 np.savez({out!r}, **res)
 """
     subprocess.run([sys.executable, "-c", code], check=True, timeout=300)
