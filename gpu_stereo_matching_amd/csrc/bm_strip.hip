@@ -1,20 +1,26 @@
-// bm_strip.hip — box matching at radius 16..31 with the disparities across the lanes (round 6).
+// bm_strip.hip — box matching at radius 16..25 with the disparities across the lanes (round 6).
 //
 // The fused tile kernel (bm_box.hip) keeps TW = 64 - 2r output columns per 64-lane tile and stops at r = 15; the
 // separable path (bm_wide.hip) streams a u16 plane of vertical sums per d through HBM (2 B written + 2 B read per
 // (pixel, d)) at any r.  This kernel keeps the vertical sums on chip instead, for the radii just past the tile
 // kernel: one workgroup walks a band of rows of a 128-column strip, lane = disparity (d_lo + 64 * wave + lane), and
-// each lane holds V_d(c) = sum of AD_d over the rows y-r..y+r for all 128 columns of the strip in registers (u16
-// pairs, V <= 63 * 255).  Per row step, for its d:
+// each lane holds V_d(c) = sum of AD_d over the rows y-r..y+r for all 128 columns of the strip in 64 registers (u16
+// pairs of adjacent columns, V <= 51 * 255).  Per row step, for its d:
 //   V_d(c) += AD_d(y + r, c) - AD_d(y - r - 1, c)      (Device.cu:27-31; rows outside the frame are 0)
-//   S_d(x) = sum of V_d over c = x-r..x+r              (running sum along the strip, Device.cu:46-56)
-//   key = S << 8 | d, min over the lanes by a butterfly of DPP / swizzle / bpermute exchanges that leaves lane i
-//   of every 8 with the minimum of output i of each group of 8, then over the waves through LDS, with the 50 win^2
-//   seed (Device.cu:37) and the validity d <= W - x (:44): the WTA of getDisp, bit for bit.
-// The strip's L and R rows of the step are staged in LDS by the workgroup (double-buffered: the next step's rows
-// load while this one computes): L spread to u16 pairs once per row, R as bytes (each lane reads its 4-byte
-// window at column c - d with v_alignbyte).  Nothing but the pair and the map touches HBM.
-// Output columns per strip: 128 - 2r (r = 16: 96, r = 31: 66); a band's first 2r row steps only build V.
+//   S_d(x) = sum of V_d over c = x-r..x+r              (running sum along the strip, SDWA adds, Device.cu:46-56)
+//   key = S << 8 | d, min over the 64 lanes by a transpose-reduce butterfly (permlane32 / permlane16 swaps, a DPP
+//   half-row exchange, three DPP steps within 8 lanes: 18 VALU per 8 outputs, no LDS), then over the waves through
+//   LDS, with the 50 win^2 seed (Device.cu:37) and the validity d <= W - x (:44): the WTA of getDisp, bit for bit.
+// The step's L and R rows (the row entering V and the row leaving it) are staged in LDS as u16 pairs: L once, R in
+// two copies one column apart so that every lane reads aligned words whatever the parity of its offset DP - d
+// (copy stride = 16 mod 32 words: conflict-free).  Their global loads are issued two steps ahead into registers,
+// written to LDS one step ahead (double buffer), so no step waits on memory.  Nothing but the pair and the map
+// touches HBM.  Interior strips run an unmasked body; the strips at the frame's edges (columns below d or past W,
+// outputs past W or with d > W - x) a masked copy.
+// Output columns per strip: 128 - 2r (r = 16: 96, r = 25: 78); a band's first 2r row steps only build V.  Bands:
+// as many as the resident workgroups allow in one round (4 waves per SIMD: <= 128 VGPRs).
+// 1080p, D = 128, 8 frames per call (us per frame, MI355X, same box): r = 16 189.9 / r = 20 203.2 / r = 25 225.6
+// against the separable path's 234.6 / 235.3 / 237.5.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -33,6 +39,18 @@ constexpr int kNT = 256;      // max threads per workgroup (4 waves: d spans up 
 #endif
 #ifndef SM_STRIP_LA
 #define SM_STRIP_LA 1         // 4-column groups whose LDS reads are in flight ahead of the one being summed
+#endif
+#ifndef SM_STRIP_ADOR
+#define SM_STRIP_ADOR 1       // |a - b| as (a -sat b) | (b -sat a) (2 % faster than max - min at r = 20)
+#endif
+#ifndef SM_STRIP_CH2
+#define SM_STRIP_CH2 0        // 1: the row's window sums as two independent chains (first / second half of the groups)
+#endif
+#ifndef SM_STRIP_VMASK
+#define SM_STRIP_VMASK 1
+#endif
+#ifndef SM_STRIP_ONELOOP
+#define SM_STRIP_ONELOOP 0
 #endif
 // every lambda of the kernel inlined: one left out of line takes V (captured by reference) to scratch
 #define SM_INL __attribute__((always_inline))
@@ -69,7 +87,8 @@ constexpr int stage_bytes(int RS) { return 2 * kSP * 4 + 2 * 2 * RS * 4; }
 
 template <int R>
 __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                    int64_t fstride, int W, int H, int pitch, int d_lo, int d_hi, int BH,
+                                                    int64_t fstride, int W, int H, int pitch, int d_lo, int d_hi, int EL,
+                                                    int NI, int nb, int nbe,
                                                     int DP, int RW, int RS, int nw, uint32_t seed, uint32_t thresh,
                                                     uint8_t* __restrict__ disp, int opitch, int64_t ostride,
                                                     uint32_t* __restrict__ keys) {
@@ -80,7 +99,30 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     const int nt = 64 * nw;                    // threads (blockDim.x, kept in an SGPR)
     uint32_t* wmin = reinterpret_cast<uint32_t*>(lds + 2 * BUF);   // [2][nw][NG * 8]
 
-    const int strip = blockIdx.x, band = blockIdx.y, f = blockIdx.z;
+    // blockIdx.x runs over the (strip, band) pairs of a frame: the EL left edge strips in nbe bands each, the NI
+    // interior strips in nb bands, the remaining (right edge) strips in nbe bands.  The edge strips' masked body
+    // costs more per row, so their bands are shorter: every workgroup of the one round finishes at about the same time
+    const int f = blockIdx.z;
+    int strip, band, bands;
+    {
+        const int b = blockIdx.x, e0 = EL * nbe, i0 = e0 + NI * nb;
+        if (b < e0) {
+            strip = b / nbe;
+            band = b - strip * nbe;
+            bands = nbe;
+        } else if (b < i0) {
+            const int k = (b - e0) / nb;
+            strip = EL + k;
+            band = b - e0 - k * nb;
+            bands = nb;
+        } else {
+            const int k = (b - i0) / nbe;
+            strip = EL + NI + k;
+            band = b - i0 - k * nbe;
+            bands = nbe;
+        }
+    }
+    const int BH = (H + bands - 1) / bands;
     const int x0 = strip * SW, cs0 = x0 - R, rb0 = cs0 - DP;
     const int y0 = band * BH, y1 = min(y0 + BH, H);
     const uint8_t* Lf = Limg + (int64_t)f * fstride;
@@ -100,7 +142,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     const bool out_ok = x0 + SW <= W && (d_hi - 1) <= W - (x0 + SW - 1);
 
     // L: [2][kSP] words (L(2p), L(2p + 1)); R: [2 rows][2 copies][RS] words, copy 0 word i = (R(rb0 + 2i),
-    // R(rb0 + 2i + 1)), copy 1 the same one column on, so that every lane reads aligned words whatever d's parity
+    // R(rb0 + 2i + 1)), copy 1 one column back (R(rb0 + 2i - 1), R(rb0 + 2i)), so that every lane reads aligned words whatever d's parity
     // item e of a step: e < nL one 4-column group of the L rows (in, out), else one of the R rows.  The loads of
     // step s + 2 are issued in step s into registers (kPF items per thread) and written to LDS in step s + 1, so
     // no step waits on a global load
@@ -123,7 +165,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
                 const int j = io ? e2 - ng : e2;
                 const int y = io ? yout : yin;
                 pw[i] = ld4(Rf, y, rb0 + 4 * j, W, H, pitch);
-                pw2[i] = ld4(Rf, y, rb0 + 4 * j + 4, W, H, pitch);
+                pw2[i] = ld4(Rf, y, rb0 + 4 * j - 4, W, H, pitch);
             }
         }
     };
@@ -146,7 +188,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
                 *reinterpret_cast<uint2*>(row) =
                     make_uint2(__builtin_amdgcn_perm(0u, w, 0x0c010c00u), __builtin_amdgcn_perm(0u, w, 0x0c030c02u));
                 *reinterpret_cast<uint2*>(row + RS) =
-                    make_uint2(__builtin_amdgcn_perm(0u, w, 0x0c020c01u), __builtin_amdgcn_perm(w2, w, 0x0c040c03u));
+                    make_uint2(__builtin_amdgcn_perm(w, w2, 0x0c040c03u), __builtin_amdgcn_perm(0u, w, 0x0c020c01u));
             }
         }
     };
@@ -154,7 +196,8 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     // this lane's R window: strip column c reads R(cs0 + c - d) = staged column DP - d + c of copy 0
     const int ro = DP - d;                      // >= 0 (DP >= d_hi - 1 >= d for the lanes that count)
     const int roc = ro < 0 ? 0 : ro;            // lanes past the slice read in range
-    const int rword = (roc >> 1) + (roc & 1) * RS;
+    // (odd: copy 1 word (roc + 1) / 2; with RS = 16 mod 32 the 32 lanes of a read half hit 32 distinct banks)
+    const int rword = (roc >> 1) + (roc & 1) * (RS + 1);
     // AD masks for the edge strips: column c = cs0 + k counts when d <= c < W (Device.cu:27-31 and the frame)
     const int clo = d - cs0, chi = W - cs0;     // strip column index range [clo, chi)
 
@@ -170,10 +213,30 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
         const uint8_t* B = lds + buf * BUF;
         const uint2* Ls = reinterpret_cast<const uint2*>(B);       // [2][kSQ]
         const uint32_t* Rr = reinterpret_cast<const uint32_t*>(B + 2 * kSP * 4) + rword;   // row io at + io * 2 * RS
+#if SM_STRIP_VMASK
+        // edge strips: the AD is summed unmasked and V is cleared afterwards at the columns outside [clo, chi) (what
+        // they hold is never read before the next clear): 4 VALU per register and step instead of a select per
+        // column and row.  mw[i]: bit c of the 32 columns 32 i .. 32 i + 31 set where the column counts
+        uint32_t mw[4];
+        if constexpr (EDGE) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int a0 = clo - 32 * i, a1 = chi - 32 * i;
+                asm volatile("" : "+v"(a0), "+v"(a1));   // per step, not hoisted into live registers
+                a0 = min(max(a0, 0), 32);
+                a1 = min(max(a1, 0), 32);
+                const uint32_t lo = a0 >= 32 ? 0u : ~0u << a0;
+                const uint32_t hi = a1 >= 32 ? ~0u : (1u << a1) - 1u;
+                mw[i] = lo & hi;
+            }
+        }
+        int mlo = 0, mhi = 0;
+#else
         // opaque copies of the mask bounds: otherwise the column compares, loop-invariant, are hoisted out of the
         // row loop into 128 SGPR pairs and spilled
         int mlo = clo, mhi = chi;
         if constexpr (EDGE) asm volatile("" : "+v"(mlo), "+v"(mhi));
+#endif
         struct G { uint2 li, lo; uint32_t ri0, ri1, ro0, ro1; };
         auto load = [&](int q) SM_INL {
             G g;
@@ -189,8 +252,13 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
         };
         auto ad = [&](uint32_t l, uint32_t r, int c) SM_INL {
             const u16x2 a = as16(l), b = as16(r);
+#if SM_STRIP_ADOR
+            // |a - b| = (a -sat b) | (b -sat a): two packed clamped subtracts and a VOP2 or
+            u16x2 e = as16(as32(__builtin_elementwise_sub_sat(a, b)) | as32(__builtin_elementwise_sub_sat(b, a)));
+#else
             u16x2 e = __builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b);
-            if constexpr (EDGE) {
+#endif
+            if constexpr (EDGE && !SM_STRIP_VMASK) {
                 e.x = (c >= mlo && c < mhi) ? e.x : (unsigned short)0;
                 e.y = (c + 1 >= mlo && c + 1 < mhi) ? e.y : (unsigned short)0;
             }
@@ -211,6 +279,19 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
             }
             V[2 * q] = as32(v0);
             V[2 * q + 1] = as32(v1);
+#if SM_STRIP_VMASK
+            if constexpr (EDGE) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    // columns 4q + 2k, 4q + 2k + 1: bit (4q + 2k) % 32 of word q / 8, each bit to a u16 half
+                    const uint32_t w = mw[q >> 3];
+                    const int b = (4 * q + 2 * k) & 31;
+                    const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)w, b, 1);
+                    const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)w, b + 1, 1);
+                    V[2 * q + k] &= (m0 & 0xFFFFu) | (m1 & 0xFFFF0000u);
+                }
+            }
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -243,14 +324,10 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
         // output j counts when x0 + j < W and d <= W - x0 - j (opaque for the same reason as update's bounds)
         int jw = W - x0, jd = W - x0 - d;
         if constexpr (OMASK) asm volatile("" : "+v"(jw), "+v"(jd));
-        uint32_t S = s0;
-#pragma unroll
-        for (int c = 0; c < 2 * R; ++c) S = sacc(S, c, std::true_type{});
         // the groups' minima, stored after the last group: a store per group would end the basic block (the
         // 8-lane mask), serialising each group's butterfly behind the next group's window sums
         uint32_t res[NG];
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
+        auto grp = [&](uint32_t S, int g) SM_INL -> uint32_t {
             uint32_t k[8];
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
@@ -287,6 +364,27 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
             n = dpp_min<0x141>(n, n);
             n = dpp_min<0xB1>(n, n);
             res[g] = dpp_min<0x4E>(n, n);
+            return S;
+        };
+        // window sum of output 8 g0 - 1's successor: columns 8 g0 .. 8 g0 + 2R - 1
+        auto init = [&](int g0) SM_INL -> uint32_t {
+            uint32_t S = s0;
+#pragma unroll
+            for (int c = 8 * g0; c < 8 * g0 + 2 * R; ++c) S = sacc(S, c, std::true_type{});
+            return S;
+        };
+        if constexpr (SM_STRIP_CH2 != 0 && NG >= 2) {
+            constexpr int NGA = (NG + 1) / 2;
+            uint32_t SA = init(0), SB = init(NGA);
+#pragma unroll
+            for (int i = 0; i < NGA; ++i) {
+                SA = grp(SA, i);
+                if (NGA + i < NG) SB = grp(SB, NGA + i);
+            }
+        } else {
+            uint32_t S = init(0);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) S = grp(S, g);
         }
         if ((lane & 7) == 0) {
             uint32_t* wm = wmin + (wb * nw + wave) * (NG * 8) + (lane >> 3);
@@ -329,8 +427,8 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     }
     __syncthreads();
 #ifdef SM_STRIP_PROF
-    // timing-only instrumentation: shader-clock cycles per phase of the phase-B steps, summed per wave; block
-    // (0, 0, 0)'s wave 0 writes them over its first map bytes at the end
+    // timing-only instrumentation: shader-clock cycles per phase over all steps, summed per wave; block
+    // (SM_STRIP_PROF_X, 0, 0)'s wave 0 writes them over the first map bytes of frame 0 at the end
     uint64_t prof[5] = {0, 0, 0, 0, 0};
 #define SM_STAMP(v) do { __builtin_amdgcn_sched_barrier(0); v = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
@@ -351,7 +449,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
         SM_STAMP(t1);
         if (!(SM_STRIP_SKIP & 2)) update(buf, edge, with_out);
         SM_STAMP(t2);
-        if constexpr (decltype(with_out)::value) {
+        if (decltype(with_out)::value && (SM_STRIP_ONELOOP == 0 || st >= 2 * R)) {
             if (!(SM_STRIP_SKIP & 4)) {
                 const int wb = (st - 2 * R) & 1;
                 row_wta(wb, edge);                                // the masked keys go with the masked columns
@@ -364,7 +462,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
 #ifdef SM_STRIP_PROF
         uint64_t t5;
         SM_STAMP(t5);
-        if constexpr (decltype(with_out)::value) {
+        {
             prof[0] += t1 - t0;
             prof[1] += t2 - t1;
             prof[2] += t3 - t2;
@@ -374,16 +472,22 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
 #endif
     };
     // the edge strips (columns outside the frame or below d, outputs past W or with invalid d) take the masked body
+    // SM_STRIP_ONELOOP: one loop body for every step (the first 2R subtract staged zero rows: a third less code, but
+    // 8 % slower at r = 20), else a separate add-only loop for them
     auto run = [&](auto edge) SM_INL {
         int st = 0;
-        for (; st < 2 * R; ++st) step(st, edge, std::false_type{});
+        if constexpr (SM_STRIP_ONELOOP == 0)
+            for (; st < 2 * R; ++st) step(st, edge, std::false_type{});
         for (; st < nsteps; ++st) step(st, edge, std::true_type{});
     };
     if (col_ok && out_ok) run(std::false_type{});
     else run(std::true_type{});
     emit((nsteps - 1 - 2 * R) & 1, y1 - 1);
 #ifdef SM_STRIP_PROF
-    if (disp && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0) {
+#ifndef SM_STRIP_PROF_X
+#define SM_STRIP_PROF_X 0
+#endif
+    if (disp && blockIdx.x == SM_STRIP_PROF_X && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0) {
         __syncthreads();
         for (int i = 0; i < 5; ++i) __builtin_memcpy(disp + 8 * i, &prof[i], 8);
     }
@@ -407,14 +511,50 @@ int device_cus() {
     return n;
 }
 
-// frames x bands x strips, one round of workgroups: as many row bands as the resident workgroups allow (a second,
-// partial round would leave most of the chip idle while it runs), each at least 4r rows tall (a band re-walks the
-// 2r rows above its first output)
-int strip_bands(int H, int R, int strips, int frames, int resident) {
-    const int64_t cols = (int64_t)strips * frames;
-    int nb = (int)std::max<int64_t>(1, resident / cols);
-    nb = std::min(nb, std::max(1, H / (4 * R)));
-    return nb;
+// Row bands, one round of workgroups (a second, partial round would leave most of the chip idle while it runs):
+// interior strips in nb bands, edge strips in nbe, chosen to minimise the longer of the two band walks, a band of
+// height h costing (h + 2r) row steps (its first 2r steps only build V), an edge step SM_STRIP_EDGE_COST % of an
+// interior one (the masked body), over the (nb, nbe) whose workgroups all fit at once.
+#ifndef SM_STRIP_EDGE_COST
+#define SM_STRIP_EDGE_COST 160
+#endif
+#ifndef SM_STRIP_FILL
+#define SM_STRIP_FILL 100   // percent of the resident workgroups the bands aim at
+#endif
+struct StripGrid {
+    int EL, NI, ER;   // left edge, interior and right edge strips
+    int nb, nbe;      // bands per interior / edge strip
+};
+
+StripGrid strip_grid(const MatchArgs& a, int R, int SW, int frames, int resident) {
+    StripGrid g{0, 0, 0, 1, 1};
+    const int strips = (a.W + SW - 1) / SW;
+    // the kernel's col_ok && out_ok, per strip: the interior strips are one contiguous run
+    auto interior = [&](int st) {
+        const int x0 = st * SW, cs0 = x0 - R;
+        return cs0 >= a.d_hi - 1 && cs0 + kSC <= a.W && x0 + SW <= a.W && (a.d_hi - 1) <= a.W - (x0 + SW - 1);
+    };
+    while (g.EL < strips && !interior(g.EL)) ++g.EL;
+    g.NI = 0;
+    while (g.EL + g.NI < strips && interior(g.EL + g.NI)) ++g.NI;
+    g.ER = strips - g.EL - g.NI;
+    const int ne = g.EL + g.ER;
+    const int nb_max = std::max(1, a.H / (4 * R)), nbe_max = std::max(1, a.H / (2 * R));
+    int64_t best = -1;
+    for (int nb = 1; nb <= (g.NI ? nb_max : 1); ++nb)
+        for (int nbe = 1; nbe <= (ne ? nbe_max : 1); ++nbe) {
+            const int64_t blocks = ((int64_t)ne * nbe + (int64_t)g.NI * nb) * frames;
+            if (blocks > resident && !(nb == 1 && nbe == 1)) continue;
+            const int64_t ti = g.NI ? (int64_t)((a.H + nb - 1) / nb + 2 * R) * 100 : 0;
+            const int64_t te = ne ? (int64_t)((a.H + nbe - 1) / nbe + 2 * R) * SM_STRIP_EDGE_COST : 0;
+            const int64_t t = std::max(ti, te);
+            if (best < 0 || t < best) {
+                best = t;
+                g.nb = nb;
+                g.nbe = nbe;
+            }
+        }
+    return g;
 }
 
 template <int R>
@@ -423,20 +563,17 @@ hipError_t launch_strip_r(const MatchArgs& a, int batch, hipStream_t s) {
     const int nd = a.d_hi - a.d_lo;
     const int nw = (nd + 63) / 64;
     const int DP = ((a.d_hi - 1) + 3) & ~3;
-    const int strips = (a.W + SW - 1) / SW;
     const int RW = r_words(DP, a.d_lo), RS = r_stride(RW);
     const size_t lds = (size_t)2 * stage_bytes(RS) + (size_t)2 * nw * ((SW + 7) / 8) * 8 * 4;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, strip_kernel<R>, 64 * nw, lds) != hipSuccess || per_cu <= 0)
         per_cu = 1;
-#ifndef SM_STRIP_FILL
-#define SM_STRIP_FILL 100   // percent of the resident workgroups the bands aim at
-#endif
-    const int nb = strip_bands(a.H, R, strips, batch, per_cu * device_cus() * SM_STRIP_FILL / 100);
-    const int BH = (a.H + nb - 1) / nb;
-    hipLaunchKernelGGL((strip_kernel<R>), dim3((unsigned)strips, (unsigned)nb, (unsigned)batch), dim3(64 * nw), lds, s,
-                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, BH, DP, RW, RS, nw, a.seed_key,
-                       a.thresh_key, a.disp, a.out_pitch, a.out_frame_stride, a.keys);
+    const StripGrid g = strip_grid(a, R, SW, batch, per_cu * device_cus() * SM_STRIP_FILL / 100);
+    const int64_t nblk = (int64_t)(g.EL + g.ER) * g.nbe + (int64_t)g.NI * g.nb;
+    if (nblk > 0x7FFFFFFF || batch > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((strip_kernel<R>), dim3((unsigned)nblk, 1u, (unsigned)batch), dim3(64 * nw), lds, s,
+                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, g.EL, g.NI, g.nb, g.nbe, DP,
+                       RW, RS, nw, a.seed_key, a.thresh_key, a.disp, a.out_pitch, a.out_frame_stride, a.keys);
     return hipGetLastError();
 }
 

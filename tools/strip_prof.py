@@ -17,5 +17,5 @@ torch.cuda.synchronize()
 c = out[0].flatten()[:40].cpu().numpy().view(np.uint64)
 names = ["stage", "update", "row_wta", "emit", "barrier"]
 tot = int(c.sum())
-print("phase-B cycles per wave (block 0):", {n: int(v) for n, v in zip(names, c)}, "total", tot)
+print("cycles per wave over all steps:", {n: int(v) for n, v in zip(names, c)}, "total", tot)
 print("fractions:", {n: round(int(v) / max(tot, 1), 3) for n, v in zip(names, c)})
