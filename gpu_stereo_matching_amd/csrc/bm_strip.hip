@@ -1,11 +1,11 @@
-// bm_strip.hip — box matching at radius 16..25 with the disparities across the lanes (round 6).
+// bm_strip.hip — box matching at radius 16..37 with the disparities across the lanes (round 6).
 //
 // The fused tile kernel (bm_box.hip) keeps TW = 64 - 2r output columns per 64-lane tile and stops at r = 15; the
 // separable path (bm_wide.hip) streams a u16 plane of vertical sums per d through HBM (2 B written + 2 B read per
 // (pixel, d)) at any r.  This kernel keeps the vertical sums on chip instead, for the radii just past the tile
 // kernel: one workgroup walks a band of rows of a 128-column strip, lane = disparity (d_lo + 64 * wave + lane), and
 // each lane holds V_d(c) = sum of AD_d over the rows y-r..y+r for all 128 columns of the strip in 64 registers (u16
-// pairs of adjacent columns, V <= 51 * 255).  Per row step, for its d:
+// pairs of adjacent columns, V <= 75 * 255).  Per row step, for its d:
 //   V_d(c) += AD_d(y + r, c) - AD_d(y - r - 1, c)      (Device.cu:27-31; rows outside the frame are 0)
 //   S_d(x) = sum of V_d over c = x-r..x+r              (running sum along the strip, SDWA adds, Device.cu:46-56)
 //   key = S << 8 | d, min over the 64 lanes by a transpose-reduce butterfly (permlane32 / permlane16 swaps, a DPP
@@ -17,10 +17,10 @@
 // written to LDS one step ahead (double buffer), so no step waits on memory.  Nothing but the pair and the map
 // touches HBM.  Interior strips run an unmasked body; the strips at the frame's edges (columns below d or past W,
 // outputs past W or with d > W - x) a masked copy.
-// Output columns per strip: 128 - 2r (r = 16: 96, r = 25: 78); a band's first 2r row steps only build V.  Bands:
+// Output columns per strip: 128 - 2r (r = 16: 96, r = 37: 54); a band's first 2r row steps only build V.  Bands:
 // as many as the resident workgroups allow in one round (4 waves per SIMD: <= 128 VGPRs).
-// 1080p, D = 128, 8 frames per call (us per frame, MI355X, same box): r = 16 189.9 / r = 20 203.2 / r = 25 225.6
-// against the separable path's 234.6 / 235.3 / 237.5.
+// 1080p, D = 128, 8 frames per call (us per frame, MI355X, same box, against the separable path's 234-237):
+// r = 16 141.9, r = 20 150.7, r = 25 180.2, r = 31 203.9, r = 37 223.4.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -516,7 +516,7 @@ int device_cus() {
 // height h costing (h + 2r) row steps (its first 2r steps only build V), an edge step SM_STRIP_EDGE_COST % of an
 // interior one (the masked body), over the (nb, nbe) whose workgroups all fit at once.
 #ifndef SM_STRIP_EDGE_COST
-#define SM_STRIP_EDGE_COST 160
+#define SM_STRIP_EDGE_COST 150
 #endif
 #ifndef SM_STRIP_FILL
 #define SM_STRIP_FILL 100   // percent of the resident workgroups the bands aim at

@@ -1,8 +1,8 @@
-"""GPU parity for the strip kernel (bm_strip.hip): box matching at radius 16..25 without the right view, lanes =
+"""GPU parity for the strip kernel (bm_strip.hip): box matching at radius 16..37 without the right view, lanes =
 disparities, vertical sums in registers.  Every map and slice-key array equals the oracle's getDisp
 (Device.cu:27-63) bit for bit: every radius the kernel is instantiated for, edge strips (d > x, the last strip
 past W), several row bands, frames in a batch, d-slices starting past 0, tie-heavy textures and the key
-headroom at r = 25."""
+headroom at r = 37."""
 import numpy as np
 import pytest
 
@@ -22,9 +22,9 @@ def matcher(sm):
     m.close()
 
 
-@pytest.mark.parametrize("r", list(range(16, 27)))
+@pytest.mark.parametrize("r", list(range(16, 39)))
 def test_strip_every_radius(matcher, oracle, r):
-    """Every instantiated radius, and r = 26, the first past the strip range (the separable path)."""
+    """Every instantiated radius, and r = 38, the first past the strip range (the separable path)."""
     rng = np.random.default_rng(7000 + r)
     W = int(rng.integers(4, 400))
     H = int(rng.integers(1, 160))
@@ -33,10 +33,10 @@ def test_strip_every_radius(matcher, oracle, r):
     assert np.array_equal(matcher.match(L, R, r, D), oracle.box_disp(L, R, r, D)), (W, H, D)
 
 
-@pytest.mark.parametrize("W,H,r,D", [(96, 700, 19, 24), (1000, 333, 25, 256), (130, 64, 16, 192), (78, 90, 25, 100),
-                                     (79, 90, 25, 100), (4, 3, 16, 5), (255, 1, 24, 64)])
+@pytest.mark.parametrize("W,H,r,D", [(96, 700, 19, 24), (1000, 333, 37, 256), (130, 64, 16, 192), (54, 90, 37, 100),
+                                     (55, 90, 37, 100), (4, 3, 16, 5), (255, 1, 24, 64)])
 def test_strip_shapes(matcher, oracle, W, H, r, D):
-    """A tall frame over 8 bands; exactly one / just past one strip of 78 outputs; 4 waves of d; a 4-column frame;
+    """A tall frame over 8 bands; exactly one / just past one strip of 54 outputs; 4 waves of d; a 4-column frame;
     a single row."""
     L, R = oracle.synth_pair(W + 3 * H + r, W, H, max(D, 16))
     assert np.array_equal(matcher.match(L, R, r, D), oracle.box_disp(L, R, r, D))
@@ -45,17 +45,17 @@ def test_strip_shapes(matcher, oracle, W, H, r, D):
 def test_strip_ties(matcher, oracle):
     """0/1 textures: most windows tie on cost, the smallest d wins as in the key MIN."""
     rng = np.random.default_rng(31)
-    for r, D in ((16, 40), (25, 130)):
+    for r, D in ((16, 40), (25, 130), (37, 70)):
         L = rng.integers(0, 2, (120, 300), dtype=np.uint8)
         R = rng.integers(0, 2, (120, 300), dtype=np.uint8)
         assert np.array_equal(matcher.match(L, R, r, D), oracle.box_disp(L, R, r, D)), r
 
 
-def test_strip_key_headroom_r25(matcher, oracle):
-    """AD 255 everywhere: V = 51 * 255 in each u16 half, S = 51^2 * 255 < 2^24 (key << 8 in range)."""
-    Lf = np.full((140, 200), 255, np.uint8)
-    Rz = np.zeros((140, 200), np.uint8)
-    assert np.array_equal(matcher.match(Lf, Rz, 25, 9), oracle.box_disp(Lf, Rz, 25, 9))
+def test_strip_key_headroom_r37(matcher, oracle):
+    """AD 255 everywhere: V = 75 * 255 in each u16 half, S = 75^2 * 255 < 2^24 (key << 8 in range)."""
+    Lf = np.full((160, 200), 255, np.uint8)
+    Rz = np.zeros((160, 200), np.uint8)
+    assert np.array_equal(matcher.match(Lf, Rz, 37, 9), oracle.box_disp(Lf, Rz, 37, 9))
 
 
 def test_strip_device_batch(matcher, oracle):
