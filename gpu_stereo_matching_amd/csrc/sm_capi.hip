@@ -326,7 +326,7 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
     } else if (wide) {
-        // r 16..31 without the right view: the strip kernel (bm_strip.hip), no V-plane workspace
+        // r 16..37 without the right view: the strip kernel (bm_strip.hip), no V-plane workspace
         if (!lr && sm::strip_path(a)) {
             SM_HIP(sm::launch_box_match_strip(a, batch, s));
         } else {
@@ -335,6 +335,10 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
             SM_HIP(sm::launch_box_match_wide(a, batch, reinterpret_cast<uint16_t*>(h->d_vol), lr ? right_map : nullptr,
                                              W, P, s));
         }
+    } else if (radius > sm::kMaxBoxRadius && sm::strip_path(a)) {
+        // frames past the separable path's limits (wider than 4096 columns): the strip kernel has none; the
+        // mirrored right view (valid_mode 1) below keeps the direct kernel
+        SM_HIP(sm::launch_box_match_strip(a, batch, s));
     } else {
         SM_HIP(sm::launch_box_match(a, batch, s));
     }
@@ -779,7 +783,7 @@ int slice_keys_pass(sm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, i
     a.thresh_key = seed_key(radius);
     a.keys = keys;
     if (!rkeys) {
-        if (sm::wide_path(radius, W, H, pitch) && sm::strip_path(a)) {   // r 16..31: the strip kernel (bm_strip.hip)
+        if (sm::strip_path(a)) {   // r 16..37: the strip kernel (bm_strip.hip), at any width
             SM_HIP(sm::launch_box_match_strip(a, 1, s));
             return SM_OK;
         }

@@ -328,11 +328,12 @@ def test_two_streams_one_handle(matcher, oracle, torch):
         assert np.array_equal(o.cpu().numpy(), w)
 
 
-def test_two_streams_one_handle_wide(matcher, oracle, torch):
-    """a plain box pass at r 16..127 (no LR, no median) writes the wide path's V planes into the
+@pytest.mark.parametrize("r", [20, 40])
+def test_two_streams_one_handle_wide(matcher, oracle, torch, r):
+    """a plain box pass at r 38..127 (no LR, no median) writes the separable path's V planes into the
     handle's volume workspace and may grow it; two streams on one handle are ordered, so both maps are
-    exact.  The second pair has the larger D, so its pass grows the workspace behind the first."""
-    r = 20
+    exact.  The second pair has the larger D, so its pass grows the workspace behind the first.  r = 20 runs the
+    strip kernel (no workspace) under the same ordering."""
     cfg = [(700, 300, 64, 71), (900, 400, 160, 72)]
     pairs = [oracle.synth_pair(seed, W, H, D) for W, H, D, seed in cfg]
     want = [oracle.box_disp(L, R, r, D) for (L, R), (_, _, D, _) in zip(pairs, cfg)]
