@@ -95,7 +95,8 @@ hipError_t launch_box_match_wide(const MatchArgs& a, int batch, uint16_t* ws, ui
 // like the unsigned keys at every radius (a wide window's key reaches 255 * 255^2 << 8 > 2^31 from r = 91), and
 // "no d of the slice reaches u" (0xFFFFFFFF before the flip) is INT32_MAX, as for the guided keys.
 constexpr uint32_t kRightKeyFlip = 0x80000000u;
-// radius 16..37 without the right view (bm_strip.hip): disparities across the lanes, vertical sums in registers,
+// radius 16..37 without the right view (bm_strip.hip; valid_mode 0 or 1, the mirrored right-view pass of frames
+// wider than the separable path takes): disparities across the lanes, vertical sums in registers,
 // no workspace; strip_path says whether a pass takes it (SM_WIDE_STRIP=0, read once, turns it off for A/B).  Past
 // r = 37 the strip's 128 - 2r outputs per 128 summed columns make it slower than the separable path (1080p D=128,
 // us per frame: r = 37 223.4 vs 236.3, r = 40 256.6 vs 236.6)

@@ -88,7 +88,7 @@ constexpr int stage_bytes(int RS) { return 2 * kSP * 4 + 2 * 2 * RS * 4; }
 template <int R>
 __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t fstride, int W, int H, int pitch, int d_lo, int d_hi, int EL,
-                                                    int NI, int nb, int nbe,
+                                                    int NI, int nb, int nbe, int vm,
                                                     int DP, int RW, int RS, int nw, uint32_t seed, uint32_t thresh,
                                                     uint8_t* __restrict__ disp, int opitch, int64_t ostride,
                                                     uint32_t* __restrict__ keys) {
@@ -139,7 +139,8 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     // strip-uniform: every column of the strip >= every d and inside the frame (no AD masks), and every output
     // inside the frame with every d valid (no key masks)
     const bool col_ok = cs0 >= d_hi - 1 && cs0 + kSC <= W;
-    const bool out_ok = x0 + SW <= W && (d_hi - 1) <= W - (x0 + SW - 1);
+    // (vm = valid_mode: 0 d <= W - x, Device.cu:44; 1 the mirrored right view's d <= x)
+    const bool out_ok = x0 + SW <= W && (vm == 0 ? (d_hi - 1) <= W - (x0 + SW - 1) : (d_hi - 1) <= x0);
 
     // L: [2][kSP] words (L(2p), L(2p + 1)); R: [2 rows][2 copies][RS] words, copy 0 word i = (R(rb0 + 2i),
     // R(rb0 + 2i + 1)), copy 1 one column back (R(rb0 + 2i - 1), R(rb0 + 2i)), so that every lane reads aligned words whatever d's parity
@@ -321,9 +322,10 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     // the row's S, keys and the wave minimum of each output; lane 8i of group g stores output 8g + i's minimum
     auto row_wta = [&](int wb, auto omask) SM_INL {
         constexpr bool OMASK = decltype(omask)::value;
-        // output j counts when x0 + j < W and d <= W - x0 - j (opaque for the same reason as update's bounds)
-        int jw = W - x0, jd = W - x0 - d;
-        if constexpr (OMASK) asm volatile("" : "+v"(jw), "+v"(jd));
+        // output j counts when x0 + j < W and jl <= j <= jd: d <= W - x0 - j (vm 0) or d <= x0 + j (vm 1); opaque
+        // for the same reason as update's bounds
+        int jw = W - x0, jd = vm == 0 ? W - x0 - d : (1 << 30), jl = vm == 0 ? -(1 << 30) : d - x0;
+        if constexpr (OMASK) asm volatile("" : "+v"(jw), "+v"(jd), "+v"(jl));
         // the groups' minima, stored after the last group: a store per group would end the basic block (the
         // 8-lane mask), serialising each group's butterfly behind the next group's window sums
         uint32_t res[NG];
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
                 if (j < SW) {
                     S = sacc(S, j + 2 * R, std::true_type{});
                     uint32_t key = (S << 8) | dd;
-                    if constexpr (OMASK) key = (j < jw && j <= jd) ? key | dmask : 0xFFFFFFFFu;   // Device.cu:44
+                    if constexpr (OMASK) key = (j < jw && j <= jd && j >= jl) ? key | dmask : 0xFFFFFFFFu;   // Device.cu:44
                     k[m] = key;
                     S = sacc(S, j, std::false_type{});
                 } else {
@@ -532,7 +534,8 @@ StripGrid strip_grid(const MatchArgs& a, int R, int SW, int frames, int resident
     // the kernel's col_ok && out_ok, per strip: the interior strips are one contiguous run
     auto interior = [&](int st) {
         const int x0 = st * SW, cs0 = x0 - R;
-        return cs0 >= a.d_hi - 1 && cs0 + kSC <= a.W && x0 + SW <= a.W && (a.d_hi - 1) <= a.W - (x0 + SW - 1);
+        return cs0 >= a.d_hi - 1 && cs0 + kSC <= a.W && x0 + SW <= a.W &&
+               (a.valid_mode == 0 ? (a.d_hi - 1) <= a.W - (x0 + SW - 1) : (a.d_hi - 1) <= x0);
     };
     while (g.EL < strips && !interior(g.EL)) ++g.EL;
     g.NI = 0;
@@ -572,7 +575,7 @@ hipError_t launch_strip_r(const MatchArgs& a, int batch, hipStream_t s) {
     const int64_t nblk = (int64_t)(g.EL + g.ER) * g.nbe + (int64_t)g.NI * g.nb;
     if (nblk > 0x7FFFFFFF || batch > 65535) return hipErrorInvalidValue;
     hipLaunchKernelGGL((strip_kernel<R>), dim3((unsigned)nblk, 1u, (unsigned)batch), dim3(64 * nw), lds, s,
-                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, g.EL, g.NI, g.nb, g.nbe, DP,
+                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, g.EL, g.NI, g.nb, g.nbe, a.valid_mode, DP,
                        RW, RS, nw, a.seed_key, a.thresh_key, a.disp, a.out_pitch, a.out_frame_stride, a.keys);
     return hipGetLastError();
 }
@@ -597,7 +600,7 @@ bool strip_path(const MatchArgs& a) {
         const char* e = getenv("SM_WIDE_STRIP");
         return !(e && e[0] == '0');
     }();
-    return on && a.radius >= kStripMinRadius && a.radius <= kStripMaxRadius && a.valid_mode == 0 &&
+    return on && a.radius >= kStripMinRadius && a.radius <= kStripMaxRadius && (a.valid_mode == 0 || a.valid_mode == 1) &&
            a.d_hi > a.d_lo && a.d_hi <= kMaxDisp && a.W >= 4 && a.H >= 1;
 }
 

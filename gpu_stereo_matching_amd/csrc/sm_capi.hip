@@ -336,8 +336,8 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
                                              W, P, s));
         }
     } else if (radius > sm::kMaxBoxRadius && sm::strip_path(a)) {
-        // frames past the separable path's limits (wider than 4096 columns): the strip kernel has none; the
-        // mirrored right view (valid_mode 1) below keeps the direct kernel
+        // frames past the separable path's limits (wider than 4096 columns): the strip kernel has none (the
+        // mirrored right view below takes it too)
         SM_HIP(sm::launch_box_match_strip(a, batch, s));
     } else {
         SM_HIP(sm::launch_box_match(a, batch, s));
@@ -361,7 +361,10 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
             b.disp = right_map;
             b.out_pitch = W;
             b.out_frame_stride = P;
-            SM_HIP(sm::launch_box_match(b, batch, s));
+            if (radius > sm::kMaxBoxRadius && sm::strip_path(b))   // frames wider than the separable path takes
+                SM_HIP(sm::launch_box_match_strip(b, batch, s));
+            else
+                SM_HIP(sm::launch_box_match(b, batch, s));
         }
     }
     const uint8_t* rcheck = right_map;

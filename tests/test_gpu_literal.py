@@ -167,8 +167,8 @@ def test_wide_path_bit_exact_sizes(matcher, oracle, W, H, r, D):
 
 
 def test_wide_path_fallback_past_4096_columns(oracle):
-    """Wider than 4096 columns: the strip kernel at r 16..37 (no width limit), the direct generic kernel past
-    it and for the mirrored right view of the LR check (correct, not fast)."""
+    """Wider than 4096 columns: the strip kernel at r 16..37 (no width limit; the LR check's mirrored right view
+    too, valid_mode 1), the direct generic kernel past it (correct, not fast)."""
     import gpu_stereo_matching_amd as sm
     L, R = oracle.synth_pair(9, 4100, 6, 16)
     with sm.BlockMatcher(0, 4100, 8, 16) as m:
@@ -180,6 +180,9 @@ def test_wide_path_fallback_past_4096_columns(oracle):
     L2, R2 = oracle.synth_pair(10, 5000, 90, 128)
     with sm.BlockMatcher(0, 5000, 90, 128) as m:
         assert np.array_equal(m.match(L2, R2, 24, 128), oracle.box_disp(L2, R2, 24, 128))
+        chk, rd, mask = m.match_lr(L2, R2, 17, 100)
+        _, rd_o, chk_o, mask_o = oracle.box_lr(L2, R2, 17, 100)
+        assert np.array_equal(rd, rd_o) and np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)
 
 
 @pytest.mark.parametrize("r,D", [(16, 64), (31, 48), (127, 12)])
