@@ -190,9 +190,10 @@ VARIANTS = (
     ("1080p 23x23 box d128", 1920, 1080, 128, 11, "box", False, False, 32),
     ("1080p 31x31 box d128", 1920, 1080, 128, 15, "box", False, False, 32),
     ("1080p 31x31 box+lr d128", 1920, 1080, 128, 15, "box", True, False, 32),
-    # r 16..25 without LR: the strip kernel (csrc/bm_strip.hip); with LR and r 26..127 the
-    # separable wide-window path (csrc/bm_wide.hip)
+    # r 16..37: the strip kernel (csrc/bm_strip.hip); r 38..127 the separable wide-window path
+    # (csrc/bm_wide.hip)
     ("1080p 41x41 box d128", 1920, 1080, 128, 20, "box", False, False, 8),
+    ("1080p 41x41 box+lr d128", 1920, 1080, 128, 20, "box", True, False, 8),
     ("1080p 255x255 box+lr d128", 1920, 1080, 128, 127, "box", True, False, 8),
     ("cfg5 4K 11x11 box d192", 3840, 2160, 192, 5, "box", False, False, 8),
     ("cfg5 4K 11x11 box+lr d192", 3840, 2160, 192, 5, "box", True, False, 8),

@@ -107,6 +107,10 @@ constexpr int kStripMinRadius = 16;
 constexpr int kStripMaxRadius = SM_STRIP_MAX_R;
 bool strip_path(const MatchArgs& a);
 hipError_t launch_box_match_strip(const MatchArgs& a, int batch, hipStream_t s);
+// the same with the right view (a.valid_mode 0, a.d_lo 0; bm_strip_lr.hip): right_keys [batch][H][W], filled with
+// ~0 by the caller, receives the MIN over d of (C_L(u + d, d) << 8 | d) over d <= u + d < W: the separable path's
+// right-view keys, whose low byte is dR
+hipError_t launch_box_match_strip_lr(const MatchArgs& a, int batch, uint32_t* right_keys, hipStream_t s);
 constexpr int kMaxWideWidth = 4096;
 // radius 16..127, 4 <= W <= 4096 and frames below 2^31 bytes (its buffer loads address a frame with 32-bit
 // offsets) take the separable wide-window path (bm_wide.hip); the rest the generic kernel

@@ -85,19 +85,24 @@ constexpr int r_words(int DP, int d_lo) { return (DP - (d_lo & ~3) + kSC + 4) / 
 constexpr int r_stride(int RW) { return ((RW + 15) & ~31) + 16; }
 constexpr int stage_bytes(int RS) { return 2 * kSP * 4 + 2 * 2 * RS * 4; }
 
-template <int R>
+// RIGHT: the right view too, folded per output row into an LDS row by atomic min (C_R(u, d) = C_L(u + d, d) for
+// u = x - d >= 0, StereoHelper.cpp:156-180, as the separable path's hwta kernel) and flushed into rk, the frame's
+// right keys [batch][H][W] (filled with ~0 by the caller), by global atomic min (strips overlap in u)
+template <int R, bool RIGHT>
 __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t fstride, int W, int H, int pitch, int d_lo, int d_hi, int EL,
                                                     int NI, int nb, int nbe, int vm,
                                                     int DP, int RW, int RS, int nw, uint32_t seed, uint32_t thresh,
                                                     uint8_t* __restrict__ disp, int opitch, int64_t ostride,
-                                                    uint32_t* __restrict__ keys) {
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ rk) {
     constexpr int SW = kSC - 2 * R;            // output columns of the strip
     constexpr int NG = (SW + 7) / 8;           // groups of 8 outputs
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int BUF = stage_bytes(RS);           // one step: L in/out as u16 column pairs, R in/out as two copies
     const int nt = 64 * nw;                    // threads (blockDim.x, kept in an SGPR)
     uint32_t* wmin = reinterpret_cast<uint32_t*>(lds + 2 * BUF);   // [2][nw][NG * 8]
+    const int RN = SW + DP;                    // right row: u = x0 - DP + i, i < RN
+    uint32_t* rrow = wmin + 2 * nw * NG * 8;   // [2][RN] (RIGHT)
 
     // blockIdx.x runs over the (strip, band) pairs of a frame: the EL left edge strips in nbe bands each, the NI
     // interior strips in nb bands, the remaining (right edge) strips in nbe bands.  The edge strips' masked body
@@ -324,8 +329,11 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
         constexpr bool OMASK = decltype(omask)::value;
         // output j counts when x0 + j < W and jl <= j <= jd: d <= W - x0 - j (vm 0) or d <= x0 + j (vm 1); opaque
         // for the same reason as update's bounds
-        int jw = W - x0, jd = vm == 0 ? W - x0 - d : (1 << 30), jl = vm == 0 ? -(1 << 30) : d - x0;
-        if constexpr (OMASK) asm volatile("" : "+v"(jw), "+v"(jd), "+v"(jl));
+        int jw = W - x0, jd = vm == 0 ? W - x0 - d : (1 << 30), jl = vm == 0 ? -(1 << 30) : d - x0, jr = d - x0;
+        if constexpr (OMASK) asm volatile("" : "+v"(jw), "+v"(jd), "+v"(jl), "+v"(jr));
+        // RIGHT: LDS byte address of this lane's slot for output 0 of the row buffer wb
+        [[maybe_unused]] const uint32_t rbase =
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(rrow + wb * RN + roc);
         // the groups' minima, stored after the last group: a store per group would end the basic block (the
         // 8-lane mask), serialising each group's butterfly behind the next group's window sums
         uint32_t res[NG];
@@ -337,6 +345,15 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
                 if (j < SW) {
                     S = sacc(S, j + 2 * R, std::true_type{});
                     uint32_t key = (S << 8) | dd;
+                    if constexpr (RIGHT) {
+                        // right candidate u = x - d: valid for x >= d and x < W (lanes past the slice: ~0).  An
+                        // inline ds_min_u32 with an immediate offset: the C++ atomic under a select became a
+                        // divergent branch per output (and 230 VGPRs); LDS ops complete in order, so the compiler's
+                        // own waitcnts stay conservative, and the step ends with an explicit lgkmcnt(0)
+                        uint32_t kr = key | dmask;
+                        if constexpr (OMASK) kr = (j < jw && j >= jr) ? kr : 0xFFFFFFFFu;
+                        asm volatile("ds_min_u32 %0, %1 offset:%2" : : "v"(rbase), "v"(kr), "i"(4 * j) : "memory");
+                    }
                     if constexpr (OMASK) key = (j < jw && j <= jd && j >= jl) ? key | dmask : 0xFFFFFFFFu;   // Device.cu:44
                     k[m] = key;
                     S = sacc(S, j, std::false_type{});
@@ -396,6 +413,15 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     };
     // the previous row's map: the minimum over the waves and the seed (Device.cu:37-38, 63)
     auto emit = [&](int wb, int y) SM_INL {
+        if constexpr (RIGHT) {   // the row's right candidates into the frame's right keys, the LDS row cleared
+            uint32_t* rr = rrow + wb * RN;
+            uint32_t* dst = rk + ((int64_t)f * H + y) * W + (x0 - DP);
+            for (int i = tid; i < RN; i += nt) {
+                const uint32_t v = rr[i];
+                if (v != 0xFFFFFFFFu) atomicMin(dst + i, v);   // valid keys only: 0 <= u < W
+                rr[i] = 0xFFFFFFFFu;
+            }
+        }
         for (int j = tid; j < SW; j += nt) {
             const int x = x0 + j;
             if (x >= W) continue;
@@ -423,6 +449,8 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
     rows_of(0, yi, yo);
     fetch(yi, yo);
     store(0);
+    if constexpr (RIGHT)
+        for (int i = tid; i < 2 * RN; i += nt) rrow[i] = 0xFFFFFFFFu;
     if (nsteps > 1) {
         rows_of(1, yi, yo);
         fetch(yi, yo);
@@ -460,6 +488,7 @@ __global__ __launch_bounds__(kNT, SM_STRIP_WPE) void strip_kernel(const uint8_t*
             }
         }
         SM_STAMP(t4);
+        if constexpr (RIGHT) asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");   // the inline ds_min_u32s
         __syncthreads();
 #ifdef SM_STRIP_PROF
         uint64_t t5;
@@ -560,38 +589,42 @@ StripGrid strip_grid(const MatchArgs& a, int R, int SW, int frames, int resident
     return g;
 }
 
-template <int R>
-hipError_t launch_strip_r(const MatchArgs& a, int batch, hipStream_t s) {
+template <int R, bool RIGHT>
+hipError_t launch_strip_r(const MatchArgs& a, int batch, hipStream_t s, uint32_t* rk) {
     constexpr int SW = kSC - 2 * R;
     const int nd = a.d_hi - a.d_lo;
     const int nw = (nd + 63) / 64;
     const int DP = ((a.d_hi - 1) + 3) & ~3;
     const int RW = r_words(DP, a.d_lo), RS = r_stride(RW);
-    const size_t lds = (size_t)2 * stage_bytes(RS) + (size_t)2 * nw * ((SW + 7) / 8) * 8 * 4;
+    const size_t lds = (size_t)2 * stage_bytes(RS) + (size_t)2 * nw * ((SW + 7) / 8) * 8 * 4 +
+                       (RIGHT ? (size_t)2 * (SW + DP) * 4 : 0);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, strip_kernel<R>, 64 * nw, lds) != hipSuccess || per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, strip_kernel<R, RIGHT>, 64 * nw, lds) != hipSuccess ||
+        per_cu <= 0)
         per_cu = 1;
     const StripGrid g = strip_grid(a, R, SW, batch, per_cu * device_cus() * SM_STRIP_FILL / 100);
     const int64_t nblk = (int64_t)(g.EL + g.ER) * g.nbe + (int64_t)g.NI * g.nb;
     if (nblk > 0x7FFFFFFF || batch > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((strip_kernel<R>), dim3((unsigned)nblk, 1u, (unsigned)batch), dim3(64 * nw), lds, s,
-                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, g.EL, g.NI, g.nb, g.nbe, a.valid_mode, DP,
-                       RW, RS, nw, a.seed_key, a.thresh_key, a.disp, a.out_pitch, a.out_frame_stride, a.keys);
+    hipLaunchKernelGGL((strip_kernel<R, RIGHT>), dim3((unsigned)nblk, 1u, (unsigned)batch), dim3(64 * nw), lds, s,
+                       a.left, a.right, a.frame_stride, a.W, a.H, a.pitch, a.d_lo, a.d_hi, g.EL, g.NI, g.nb, g.nbe,
+                       a.valid_mode, DP, RW, RS, nw, a.seed_key, a.thresh_key, a.disp, a.out_pitch, a.out_frame_stride,
+                       a.keys, rk);
     return hipGetLastError();
 }
 
-template <int R>
-hipError_t dispatch_strip(const MatchArgs& a, int batch, hipStream_t s) {
+template <int R, bool RIGHT>
+hipError_t dispatch_strip(const MatchArgs& a, int batch, hipStream_t s, uint32_t* rk) {
     if constexpr (R > kStripMaxRadius) {
         return hipErrorInvalidValue;
     } else {
-        if (a.radius == R) return launch_strip_r<R>(a, batch, s);
-        return dispatch_strip<R + 1>(a, batch, s);
+        if (a.radius == R) return launch_strip_r<R, RIGHT>(a, batch, s, rk);
+        return dispatch_strip<R + 1, RIGHT>(a, batch, s, rk);
     }
 }
 
 }  // namespace
 
+#ifndef SM_STRIP_RIGHT_TU
 bool strip_path(const MatchArgs& a) {
     static const bool on = [] {
 #ifdef SM_STRIP_OFF
@@ -606,7 +639,14 @@ bool strip_path(const MatchArgs& a) {
 
 hipError_t launch_box_match_strip(const MatchArgs& a, int batch, hipStream_t s) {
     if (!strip_path(a) || batch <= 0) return hipErrorInvalidValue;
-    return dispatch_strip<kStripMinRadius>(a, batch, s);
+    return dispatch_strip<kStripMinRadius, false>(a, batch, s, nullptr);
 }
+#else
+// bm_strip_lr.hip: the instantiations with the right view, compiled in their own translation unit
+hipError_t launch_box_match_strip_lr(const MatchArgs& a, int batch, uint32_t* right_keys, hipStream_t s) {
+    if (!strip_path(a) || a.valid_mode != 0 || a.d_lo != 0 || !right_keys || batch <= 0) return hipErrorInvalidValue;
+    return dispatch_strip<kStripMinRadius, true>(a, batch, s, right_keys);
+}
+#endif
 
 }  // namespace sm

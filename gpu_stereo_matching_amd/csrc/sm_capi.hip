@@ -233,6 +233,18 @@ int run_staged(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, i
 //               atomic-min row (bm_wide.hip); only frames the wide path rejects (W > 4096, or planes of
 //               2^31 bytes and up) match the mirrored pair (valid d <= x, no threshold), kept mirrored;
 //   LR check  : StereoDisparity.cpp:136-147 on the (median-filtered, :119-126) maps.
+// SM_STRIP_LR=0 (read once) keeps box + LR at r 16..37 on the separable path (A/B)
+bool strip_lr_enabled() {
+    static const bool on = [] {
+#ifdef SM_STRIP_LR_OFF
+        return false;   // A/B builds
+#endif
+        const char* e = std::getenv("SM_STRIP_LR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, int pitch, int batch,
                     int64_t fstride, int radius, int D, unsigned flags, uint8_t* disp, int opitch, int64_t ostride,
                     uint8_t* right_out, uint8_t* mask_out, int apitch, int64_t astride, hipStream_t s) {
@@ -326,9 +338,17 @@ int run_device_body(sm_handle* h, const uint8_t* L, const uint8_t* R, int W, int
         SM_HIP(sm::launch_guided_match(L, R, W, H, pitch, batch, fstride, radius, D, h->guided_eps, 0, lmap, lpitch,
                                       lstride, s));
     } else if (wide) {
-        // r 16..37 without the right view: the strip kernel (bm_strip.hip), no V-plane workspace
+        // r 16..37: the strip kernel (bm_strip.hip); without the right view it needs no workspace, with it the
+        // right keys go through the volume workspace (4 B per pixel) and their low byte is dR
         if (!lr && sm::strip_path(a)) {
             SM_HIP(sm::launch_box_match_strip(a, batch, s));
+        } else if (lr && strip_lr_enabled() && sm::strip_path(a)) {
+            int rc = ensure_vol(h, (size_t)PB * 4);
+            if (rc) return rc;
+            uint32_t* rk = reinterpret_cast<uint32_t*>(h->d_vol);
+            SM_HIP(hipMemsetAsync(rk, 0xFF, (size_t)PB * 4, s));
+            SM_HIP(sm::launch_box_match_strip_lr(a, batch, rk, s));
+            SM_HIP(sm::launch_keys_low_byte(rk, PB, right_map, s));
         } else {
             int rc = ensure_vol(h, sm::wide_workspace_bytes(W, H, D, batch));
             if (rc) return rc;

@@ -11,7 +11,7 @@ SRC=${SM_VARIANT_SRC:-gpu_stereo_matching_amd/csrc}
 OUT=tools/abv/$NAME
 mkdir -p $OUT
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Wall -Wno-unused-result $EXTRA"
-ALL="sm_capi bm_box bm_aux bm_guided bm_segtree bm_pre bm_post bm_volume bm_staged bm_rectify bm_literal bm_wide bm_strip"
+ALL="sm_capi bm_box bm_aux bm_guided bm_segtree bm_pre bm_post bm_volume bm_staged bm_rectify bm_literal bm_wide bm_strip bm_strip_lr"
 if [ -n "$SM_VARIANT_ONLY" ]; then
   for f in $ALL; do cp gpu_stereo_matching_amd/csrc/build/$f.o $OUT/$f.o; done
   ALL="$SM_VARIANT_ONLY"
