@@ -1,4 +1,4 @@
-"""GPU parity for the strip kernel (bm_strip.hip): box matching at radius 16..37 without the right view, lanes =
+"""GPU parity for the strip kernel (bm_strip.hip, right view in bm_strip_lr.hip): box matching at radius 16..37, lanes =
 disparities, vertical sums in registers.  Every map and slice-key array equals the oracle's getDisp
 (Device.cu:27-63) bit for bit: every radius the kernel is instantiated for, edge strips (d > x, the last strip
 past W), several row bands, frames in a batch, d-slices starting past 0, tie-heavy textures and the key
@@ -79,3 +79,35 @@ def test_strip_slice_keys(matcher, oracle):
         torch.cuda.synchronize()
         assert np.array_equal(k.cpu().numpy().view(np.uint32), oracle.box_keys_slice(L, R, 25, a, b)), (a, b)
     assert np.array_equal(matcher.dslice_rehearse(L, R, 25, 240, 3), oracle.box_disp(L, R, 25, 240))
+
+
+@pytest.mark.parametrize("r", [16, 22, 29, 37])
+def test_strip_lr(matcher, oracle, r):
+    """The right view folded in the strip kernel (LDS row + global atomic MIN): checked map, dR and mask equal the
+    oracle's box_lr (StereoDisparity.cpp:136-147), edge strips and D past the frame's columns included."""
+    rng = np.random.default_rng(8000 + r)
+    W = int(rng.integers(60, 700))
+    H = int(rng.integers(20, 200))
+    D = int(rng.choice([9, 64, 100, 200, 256]))
+    L, R = oracle.synth_pair(8000 + r, W, H, max(D, 16))
+    chk, rd, mask = matcher.match_lr(L, R, r, D)
+    _, rd_o, chk_o, mask_o = oracle.box_lr(L, R, r, D)
+    assert np.array_equal(rd, rd_o) and np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o), (W, H, D)
+
+
+def test_strip_lr_median_device_batch(matcher, oracle):
+    """Right keys of several frames in one launch (one right-key plane per frame), with the 7x7 median."""
+    import torch
+    r, D = 24, 80
+    pairs = [oracle.synth_pair(950 + i, 301, 97, D) for i in range(3)]
+    Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
+    Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
+    out = matcher.match_device(Lt, Rt, r, D, lr_check=True)
+    torch.cuda.synchronize()
+    for i, (L, R) in enumerate(pairs):
+        assert np.array_equal(out[i].cpu().numpy(), oracle.box_lr(L, R, r, D)[2]), i
+    L, R = pairs[0]
+    chk, rd, mask = matcher.match_lr(L, R, r, D, median=True)
+    _, cost = oracle.box_disp(L, R, r, D, want_cost=True)
+    chk_o, mask_o = oracle.lr_check(oracle.median(oracle.box_disp(L, R, r, D), 3), oracle.median(oracle.right_wta(cost), 3))
+    assert np.array_equal(chk, chk_o) and np.array_equal(mask, mask_o)

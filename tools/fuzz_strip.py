@@ -1,4 +1,4 @@
-"""Randomised parity sweep of the strip kernel (csrc/bm_strip.hip, box r 16..37 without LR) and its neighbours
+"""Randomised parity sweep of the strip kernel (csrc/bm_strip.hip, box r 16..37, LR in every other case) and its neighbours
 (r 38..40 on the separable path) against the oracle: N cases of random size, radius, d range, batch, texture and
 d-slice, every map / key array compared bit for bit.
     python tools/fuzz_strip.py [N] [seed]"""
@@ -36,9 +36,13 @@ for i in range(N):
         pairs.append((L, R))
     Lt = torch.from_numpy(np.stack([p[0] for p in pairs])).cuda()
     Rt = torch.from_numpy(np.stack([p[1] for p in pairs])).cuda()
-    out = m.match_device(Lt, Rt, r, D)
+    lr = bool(i % 2)
+    out = m.match_device(Lt, Rt, r, D, lr_check=lr)
     torch.cuda.synchronize()
-    ok = all(np.array_equal(out[b].cpu().numpy(), O.box_disp(L, R, r, D)) for b, (L, R) in enumerate(pairs))
+    if lr:
+        ok = all(np.array_equal(out[b].cpu().numpy(), O.box_lr(L, R, r, D)[2]) for b, (L, R) in enumerate(pairs))
+    else:
+        ok = all(np.array_equal(out[b].cpu().numpy(), O.box_disp(L, R, r, D)) for b, (L, R) in enumerate(pairs))
     # one d-slice of the first frame
     a = int(rng.integers(0, D))
     e = int(rng.integers(a + 1, D + 1))
@@ -47,7 +51,7 @@ for i in range(N):
     ok_k = np.array_equal(k.cpu().numpy().view(np.uint32), O.box_keys_slice(pairs[0][0], pairs[0][1], r, a, e))
     if not (ok and ok_k):
         bad += 1
-        print(f"MISMATCH case {i}: W={W} H={H} r={r} D={D} B={B} kind={kind} slice=[{a},{e}) maps={ok} keys={ok_k}",
+        print(f"MISMATCH case {i}: W={W} H={H} r={r} D={D} B={B} lr={lr} kind={kind} slice=[{a},{e}) maps={ok} keys={ok_k}",
               flush=True)
     if (i + 1) % 20 == 0:
         print(f"{i + 1} cases, {bad} mismatching", flush=True)
